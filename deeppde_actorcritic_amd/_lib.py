@@ -1,0 +1,118 @@
+"""ctypes binding of libdpac (include/dpac.h).
+
+The library is built in-tree (``make lib`` or ``__graft_entry__.build()``) and is
+loaded from this package directory.  There is no fallback: if the shared object
+is missing or fails to load, every device op raises :class:`DpacUnavailable`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DPAC_LIB", os.path.join(_HERE, "libdpac.so"))
+
+# constants mirrored from include/dpac.h
+DPAC_OK, DPAC_EINVAL, DPAC_EUNSUP = 0, -1, -2
+F32, F64 = 0, 1
+EQN_LQR, EQN_VDP, EQN_EKN, EQN_LQR_VAR = 0, 1, 2, 3
+SCHEME_NAIVE, SCHEME_ADAPTIVE = 0, 1
+TD1, TD2 = 1, 2
+COST_CRITIC, COST_ACTOR = 0, 1
+SAMPLE_NORMAL, SAMPLE_BOUNDED, SAMPLE_ZERO_X0 = 0, 1, 2
+(EVAL_DRIFT, EVAL_SIGMA, EVAL_W, EVAL_Z, EVAL_V_TRUE, EVAL_U_TRUE, EVAL_V_GRAD,
+ EVAL_B) = range(8)
+
+
+class DpacUnavailable(RuntimeError):
+    """libdpac.so is missing or could not be loaded (no CPU fallback exists)."""
+
+
+class DpacError(RuntimeError):
+    def __init__(self, func: str, code: int, msg: str):
+        super().__init__(f"{func} failed with status {code}: {msg}")
+        self.code = code
+
+
+class EqnParams(ctypes.Structure):
+    """dpac_eqn_params (include/dpac.h)."""
+
+    _fields_ = [
+        ("eqn", ctypes.c_int32), ("dim", ctypes.c_int32), ("control_dim", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("gamma", ctypes.c_double), ("R", ctypes.c_double), ("sigma_up", ctypes.c_double),
+        ("p", ctypes.c_double), ("q", ctypes.c_double), ("beta", ctypes.c_double),
+        ("k", ctypes.c_double), ("a", ctypes.c_double), ("epsilon", ctypes.c_double),
+        ("a2", ctypes.c_double), ("a3", ctypes.c_double),
+    ]
+
+
+_P = ctypes.c_void_p
+_I32, _I64, _U64, _D = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
+_EQ = ctypes.POINTER(EqnParams)
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+SIGNATURES = {
+    "dpac_abi_version": [],
+    "dpac_last_error": [],
+    "dpac_supported": [_EQ],
+    "dpac_sample": [_EQ, _I32, _I32, _I64, _I32, _U64, _I64, _P, _P, _P, _P],
+    "dpac_rollout_fwd": [_EQ, _I32, _I32, _I64, _I32, _D, _P, _P, _U64, _I64, _I32, _P, _P, _P,
+                         _P, _I32, _P, _P, _P],
+    "dpac_flag_init": [_EQ, _I32, _I32, _I64, _I32, _D, _P, _P, _P],
+    "dpac_step_fwd": [_EQ, _I32, _I32, _I64, _I32, _D, _P, _P, _P, _P, _P, _P, _I32, _P, _P, _P,
+                      _P, _P, _P, _P],
+    "dpac_step_bwd": [_EQ, _I32, _I32, _I64, _I32, _D, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _P,
+                      _P, _P, _P],
+    "dpac_td_assemble_fwd": [_EQ, _I32, _I32, _I32, _I64, _I32, _P, _P, _P, _U64, _I64, _I32, _P,
+                             _P, _P, _P, _P, _P],
+    "dpac_td_assemble_bwd": [_EQ, _I32, _I64, _I32, _P, _P, _P, _U64, _I64, _I32, _P, _P, _P, _P,
+                             _P],
+    "dpac_actor_cost_fwd": [_EQ, _I32, _I64, _I32, _P, _P, _P, _P, _P, _P, _P],
+    "dpac_equation_eval": [_EQ, _I32, _I32, _I64, _P, _P, _P, _P],
+}
+_RESTYPES = {"dpac_abi_version": ctypes.c_int32, "dpac_last_error": ctypes.c_char_p,
+             "dpac_supported": ctypes.c_int32}
+
+_lock = threading.Lock()
+_lib = None
+_load_error = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libdpac.so once; raise DpacUnavailable with the reason if impossible."""
+    global _lib, _load_error
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if _load_error is not None:
+            raise DpacUnavailable(_load_error)
+        if not os.path.exists(LIB_PATH):
+            _load_error = (f"{LIB_PATH} not found: build it with `make lib` or "
+                           "`python -c 'import __graft_entry__ as g; g.build()'`")
+            raise DpacUnavailable(_load_error)
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the host
+            _load_error = f"failed to load {LIB_PATH}: {e}"
+            raise DpacUnavailable(_load_error) from e
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = lib
+        return lib
+
+
+def call(name: str, *args) -> None:
+    """Call an entry point and raise DpacError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != DPAC_OK:
+        msg = lib.dpac_last_error()
+        raise DpacError(name, rc, msg.decode() if msg else "")
+
+
+def exported_symbols() -> list:
+    return list(SIGNATURES)

@@ -1,0 +1,433 @@
+// dpac_abi.hip — the extern "C" surface of libdpac (include/dpac.h): argument
+// validation, thread-local error reporting, dispatch to the per-equation
+// kernel instantiations, and the on-device Brownian sampler.
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "dpac_kernels.h"
+
+namespace dpac {
+int dispatch_lqr_f32(const OpArgs&);
+int dispatch_vdp_f32(const OpArgs&);
+int dispatch_ekn_f32(const OpArgs&);
+int dispatch_lqrvar_f32(const OpArgs&);
+int dispatch_lqr_f64(const OpArgs&);
+int dispatch_vdp_f64(const OpArgs&);
+int dispatch_ekn_f64(const OpArgs&);
+int dispatch_lqrvar_f64(const OpArgs&);
+bool has_dim_lqr(int);
+bool has_dim_vdp(int);
+bool has_dim_ekn(int);
+bool has_dim_lqrvar(int);
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int ok() {
+  g_err.clear();
+  return DPAC_OK;
+}
+
+int check_eq(const dpac_eqn_params* eq) {
+  if (!eq) return fail(DPAC_EINVAL, "eqn params pointer is NULL");
+  if (eq->reserved != 0) return fail(DPAC_EINVAL, "eqn params: reserved must be 0");
+  if (eq->dim < 1) return fail(DPAC_EINVAL, "dim must be >= 1 (got %d)", eq->dim);
+  switch (eq->eqn) {
+    case DPAC_EQN_LQR:
+    case DPAC_EQN_EKN:
+    case DPAC_EQN_LQR_VAR:
+      if (eq->control_dim != eq->dim)
+        return fail(DPAC_EINVAL, "control_dim (%d) must equal dim (%d) for this equation",
+                    eq->control_dim, eq->dim);
+      break;
+    case DPAC_EQN_VDP:
+      if (eq->dim != 2 * eq->control_dim)
+        return fail(DPAC_EINVAL, "VDP needs dim == 2*control_dim (dim %d, control_dim %d)",
+                    eq->dim, eq->control_dim);
+      break;
+    default:
+      return fail(DPAC_EINVAL, "unknown equation id %d", eq->eqn);
+  }
+  if (!(eq->R > 0)) return fail(DPAC_EINVAL, "R must be > 0");
+  bool has = false;
+  switch (eq->eqn) {
+    case DPAC_EQN_LQR: has = has_dim_lqr(eq->dim); break;
+    case DPAC_EQN_VDP: has = has_dim_vdp(eq->dim); break;
+    case DPAC_EQN_EKN: has = has_dim_ekn(eq->dim); break;
+    case DPAC_EQN_LQR_VAR: has = has_dim_lqrvar(eq->dim); break;
+  }
+  if (!has)
+    return fail(DPAC_EUNSUP, "equation %d has no kernel instantiation for dim %d", eq->eqn,
+                eq->dim);
+  return DPAC_OK;
+}
+
+int check_common(const dpac_eqn_params* eq, int32_t dtype, int64_t B) {
+  if (int e = check_eq(eq)) return e;
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
+  if (B < 1) return fail(DPAC_EINVAL, "num_sample must be >= 1 (got %lld)", (long long)B);
+  if (B > (int64_t)1 << 31) return fail(DPAC_EINVAL, "num_sample too large");
+  return DPAC_OK;
+}
+
+int check_time(int32_t scheme, int32_t N, double T) {
+  if (scheme != DPAC_SCHEME_NAIVE && scheme != DPAC_SCHEME_ADAPTIVE)
+    return fail(DPAC_EINVAL, "bad scheme %d", scheme);
+  if (N < 1) return fail(DPAC_EINVAL, "num_steps must be >= 1 (got %d)", N);
+  if (!(T > 0)) return fail(DPAC_EINVAL, "total_time must be > 0");
+  return DPAC_OK;
+}
+
+int check_sample_type(int32_t st) {
+  if (st != DPAC_SAMPLE_NORMAL && st != DPAC_SAMPLE_BOUNDED && st != DPAC_SAMPLE_ZERO_X0)
+    return fail(DPAC_EINVAL, "bad sample_type %d", st);
+  return DPAC_OK;
+}
+
+#define DPAC_REQUIRE(ptr) \
+  if (!(ptr)) return fail(DPAC_EINVAL, "%s: required pointer '%s' is NULL", __func__, #ptr)
+
+OpArgs blank(const dpac_eqn_params* eq, int op) {
+  OpArgs a{};
+  a.op = op;
+  a.eq = *eq;
+  return a;
+}
+
+int launch(const OpArgs& a) {
+  int r = DPAC_EUNSUP;
+  const bool f64 = a.dtype == DPAC_F64;
+  switch (a.eq.eqn) {
+    case DPAC_EQN_LQR: r = f64 ? dispatch_lqr_f64(a) : dispatch_lqr_f32(a); break;
+    case DPAC_EQN_VDP: r = f64 ? dispatch_vdp_f64(a) : dispatch_vdp_f32(a); break;
+    case DPAC_EQN_EKN: r = f64 ? dispatch_ekn_f64(a) : dispatch_ekn_f32(a); break;
+    case DPAC_EQN_LQR_VAR: r = f64 ? dispatch_lqrvar_f64(a) : dispatch_lqrvar_f32(a); break;
+  }
+  if (r == DPAC_EUNSUP) return fail(r, "no kernel for equation %d dim %d", a.eq.eqn, a.eq.dim);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
+}
+
+// ---------------------------------------------------------------------------
+// Sampler kernels (equation.py:13-44), stream layout in dpac_device.h.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int N, int D, int sample_type,
+                                                   uint64_t seed, int64_t traj_offset, T* dw) {
+  const int R = lanes_for_dim(D), C = D / R;
+  const int PB = sample_type == DPAC_SAMPLE_BOUNDED ? 4 : Rng<T>::kNormalPerBlock;
+  const int BPC = (C + PB - 1) / PB;
+  const int64_t per_row = (int64_t)R * BPC;  // counter blocks per (t, b)
+  const int64_t total = (int64_t)N * B * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t tb = i / per_row;
+    const int rem = (int)(i - tb * per_row);
+    const int r = rem / BPC, blk = rem % BPC;
+    const int t = (int)(tb / B);
+    const int64_t b = tb - (int64_t)t * B;
+    const uint64_t traj = (uint64_t)(traj_offset + b);
+    const uint64_t block = (kTagDw << 48) | ((uint64_t)t * per_row + (uint64_t)r * BPC + blk);
+    const uint4 v = philox_block(seed, traj, block);
+    T vals[4];
+    if (sample_type == DPAC_SAMPLE_BOUNDED) {
+      vals[0] = bounded_value<T>(v.x); vals[1] = bounded_value<T>(v.y);
+      vals[2] = bounded_value<T>(v.z); vals[3] = bounded_value<T>(v.w);
+    } else {
+      T n[Rng<T>::kNormalPerBlock];
+      Rng<T>::normals(v, n);
+#pragma unroll
+      for (int e = 0; e < Rng<T>::kNormalPerBlock; ++e) vals[e] = n[e];
+    }
+    T* out = dw + tb * D + r * C;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = blk * PB + e;
+      if (e < PB && j < C) out[j] = vals[e];
+    }
+  }
+}
+
+// Gaussian direction (tag) for component j of trajectory traj
+template <typename T>
+__device__ T dir_normal(uint64_t seed, uint64_t traj, uint64_t tag, int j) {
+  constexpr int PB = Rng<T>::kNormalPerBlock;
+  T n[PB];
+  Rng<T>::normals(philox_block(seed, traj, (tag << 48) | (uint64_t)(j / PB)), n);
+  const int e = j % PB;
+  T v = n[0];
+#pragma unroll
+  for (int i = 1; i < PB; ++i) v = e == i ? n[i] : v;
+  return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_sample_points(int64_t B, int D, double R,
+                                                       int sample_type, uint64_t seed,
+                                                       int64_t traj_offset, T* x0, T* x_bdry) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t traj = (uint64_t)(traj_offset + b);
+  const T Rt = (T)R;
+  if (x0) {
+    if (sample_type == DPAC_SAMPLE_ZERO_X0) {
+      for (int j = 0; j < D; ++j) x0[b * D + j] = (T)0.01;  // np.zeros + 0.01 (:39)
+    } else {
+      // r = (R*U)^(1/d) * R^((d-1)/d), U uniform (0,1]  (:14-15)
+      const uint4 v = philox_block(seed, traj, kTagRadius << 48);
+      T U;
+      if constexpr (sizeof(T) == 4) U = rocrand_device::detail::uniform_distribution(v.x);
+      else U = rocrand_device::detail::uniform_distribution_double(v.x, v.y);
+      const T r = pow(Rt * U, (T)1 / (T)D) * pow(Rt, (T)(D - 1) / (T)D);
+      T ss = 0;
+      for (int j = 0; j < D; ++j) {
+        const T g = dir_normal<T>(seed, traj, kTagDir, j);
+        ss += g * g;
+      }
+      const T nrm = sqrt(ss);
+      for (int j = 0; j < D; ++j) x0[b * D + j] = (r * dir_normal<T>(seed, traj, kTagDir, j)) / nrm;
+    }
+  }
+  if (x_bdry) {  // R * g / |g|  (:20-22)
+    T ss = 0;
+    for (int j = 0; j < D; ++j) {
+      const T g = dir_normal<T>(seed, traj, kTagBdry, j);
+      ss += g * g;
+    }
+    const T nrm = sqrt(ss);
+    for (int j = 0; j < D; ++j) x_bdry[b * D + j] = (Rt * dir_normal<T>(seed, traj, kTagBdry, j)) / nrm;
+  }
+}
+
+template <typename T>
+int sample_impl(const dpac_eqn_params* eq, int32_t sample_type, int64_t B, int32_t N,
+                uint64_t seed, int64_t off, void* x0, void* dw, void* x_bdry, hipStream_t s) {
+  const int D = eq->dim;
+  if (dw) {
+    const int R = lanes_for_dim(D), C = D / R;
+    const int PB = sample_type == DPAC_SAMPLE_BOUNDED ? 4 : Rng<T>::kNormalPerBlock;
+    const int64_t total = (int64_t)N * B * R * ((C + PB - 1) / PB);
+    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
+    const int st = sample_type == DPAC_SAMPLE_ZERO_X0 ? DPAC_SAMPLE_NORMAL : sample_type;
+    hipLaunchKernelGGL(k_sample_dw<T>, dim3((unsigned)blocks), dim3(256), 0, s, B, N, D, st, seed,
+                       off, (T*)dw);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
+  if (x0 || x_bdry) {
+    hipLaunchKernelGGL(k_sample_points<T>, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B,
+                       D, eq->R, sample_type, seed, off, (T*)x0, (T*)x_bdry);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
+  return 0;
+}
+
+}  // namespace
+}  // namespace dpac
+
+using namespace dpac;
+
+extern "C" {
+
+int32_t dpac_abi_version(void) { return DPAC_ABI_VERSION; }
+
+const char* dpac_last_error(void) { return g_err.c_str(); }
+
+int32_t dpac_supported(const dpac_eqn_params* eq) { return check_eq(eq) == DPAC_OK ? 1 : 0; }
+
+int dpac_sample(const dpac_eqn_params* eq, int32_t sample_type, int32_t dtype, int64_t num_sample,
+                int32_t num_steps, uint64_t seed, int64_t traj_offset, void* x0, void* dw,
+                void* x_bdry, void* stream) {
+  if (!eq) return fail(DPAC_EINVAL, "eqn params pointer is NULL");
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
+  if (eq->dim < 1) return fail(DPAC_EINVAL, "dim must be >= 1");
+  if (num_sample < 1) return fail(DPAC_EINVAL, "num_sample must be >= 1");
+  if (dw && num_steps < 1) return fail(DPAC_EINVAL, "num_steps must be >= 1");
+  if (int e = check_sample_type(sample_type)) return e;
+  if (traj_offset < 0) return fail(DPAC_EINVAL, "traj_offset must be >= 0");
+  hipStream_t s = (hipStream_t)stream;
+  const int r = dtype == DPAC_F64
+                    ? sample_impl<double>(eq, sample_type, num_sample, num_steps, seed,
+                                          traj_offset, x0, dw, x_bdry, s)
+                    : sample_impl<float>(eq, sample_type, num_sample, num_steps, seed,
+                                         traj_offset, x0, dw, x_bdry, s);
+  if (r) return fail(r, "sampler launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
+}
+
+int dpac_rollout_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype, int64_t num_sample,
+                     int32_t num_steps, double total_time, const void* x0, const void* dw,
+                     uint64_t seed, int64_t traj_offset, int32_t sample_type, void* x, void* dt,
+                     void* coef, void* u, int32_t cost_order, void* y, void* disc, void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (int e = check_time(scheme, num_steps, total_time)) return e;
+  DPAC_REQUIRE(x0);
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(dt);
+  DPAC_REQUIRE(coef);
+  if ((y == nullptr) != (disc == nullptr))
+    return fail(DPAC_EINVAL, "y and disc must both be given or both be NULL");
+  if (cost_order != DPAC_COST_CRITIC && cost_order != DPAC_COST_ACTOR)
+    return fail(DPAC_EINVAL, "bad cost_order %d", cost_order);
+  if (!dw) {
+    if (int e = check_sample_type(sample_type)) return e;
+    if (traj_offset < 0) return fail(DPAC_EINVAL, "traj_offset must be >= 0");
+  }
+  OpArgs a = blank(eq, OP_ROLLOUT);
+  a.scheme = scheme; a.dtype = dtype; a.B = num_sample; a.N = num_steps; a.T = total_time;
+  a.x0 = x0; a.dw = dw; a.seed = seed; a.traj_offset = traj_offset;
+  a.sample_type = sample_type == DPAC_SAMPLE_ZERO_X0 ? DPAC_SAMPLE_NORMAL : sample_type;
+  a.x_out = x; a.dt = dt; a.coef = coef; a.u_out = u; a.cost_order = cost_order; a.y = y;
+  a.disc = disc; a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+int dpac_flag_init(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype, int64_t num_sample,
+                   int32_t num_steps, double total_time, const void* x0, int32_t* flag,
+                   void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (int e = check_time(scheme, num_steps, total_time)) return e;
+  DPAC_REQUIRE(x0);
+  DPAC_REQUIRE(flag);
+  OpArgs a = blank(eq, OP_FLAG_INIT);
+  a.scheme = scheme; a.dtype = dtype; a.B = num_sample; a.N = num_steps; a.T = total_time;
+  a.x0 = x0; a.flag_out = flag; a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+int dpac_step_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype, int64_t num_sample,
+                  int32_t num_steps, double total_time, const void* x, const void* u,
+                  const void* dw_t, const int32_t* flag_in, const void* disc_in, const void* y_in,
+                  int32_t cost_order, void* x_out, int32_t* flag_out, void* disc_out, void* y_out,
+                  void* dt, void* coef, void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (int e = check_time(scheme, num_steps, total_time)) return e;
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(u);
+  DPAC_REQUIRE(dw_t);
+  DPAC_REQUIRE(flag_in);
+  DPAC_REQUIRE(x_out);
+  DPAC_REQUIRE(flag_out);
+  if (x_out == x) return fail(DPAC_EINVAL, "x_out must not alias x");
+  if (cost_order != DPAC_COST_CRITIC && cost_order != DPAC_COST_ACTOR)
+    return fail(DPAC_EINVAL, "bad cost_order %d", cost_order);
+  OpArgs a = blank(eq, OP_STEP_FWD);
+  a.scheme = scheme; a.dtype = dtype; a.B = num_sample; a.N = num_steps; a.T = total_time;
+  a.x = x; a.u = u; a.dw = dw_t; a.flag_in = flag_in; a.disc_in = disc_in; a.y_in = y_in;
+  a.cost_order = cost_order; a.x_out = x_out; a.flag_out = flag_out; a.disc_out = disc_out;
+  a.y_out = y_out; a.dt = dt; a.coef = coef; a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+int dpac_step_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype, int64_t num_sample,
+                  int32_t num_steps, double total_time, const void* x, const void* u,
+                  const void* dw_t, const int32_t* flag_in, const void* disc_in,
+                  int32_t cost_order, const void* g_x_out, const void* g_disc_out,
+                  const void* g_y_out, void* g_x, void* g_u, void* g_disc, void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (int e = check_time(scheme, num_steps, total_time)) return e;
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(u);
+  DPAC_REQUIRE(dw_t);
+  DPAC_REQUIRE(flag_in);
+  DPAC_REQUIRE(g_x_out);
+  DPAC_REQUIRE(g_x);
+  DPAC_REQUIRE(g_u);
+  if (cost_order != DPAC_COST_CRITIC && cost_order != DPAC_COST_ACTOR)
+    return fail(DPAC_EINVAL, "bad cost_order %d", cost_order);
+  OpArgs a = blank(eq, OP_STEP_BWD);
+  a.scheme = scheme; a.dtype = dtype; a.B = num_sample; a.N = num_steps; a.T = total_time;
+  a.x = x; a.u = u; a.dw = dw_t; a.flag_in = flag_in; a.disc_in = disc_in;
+  a.cost_order = cost_order; a.g_x_out = g_x_out; a.g_disc_out = g_disc_out;
+  a.g_y_out = g_y_out; a.g_x = g_x; a.g_u = g_u; a.g_disc = g_disc;
+  a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+int dpac_td_assemble_fwd(const dpac_eqn_params* eq, int32_t td_type, int32_t cost_order,
+                         int32_t dtype, int64_t num_sample, int32_t num_steps, const void* x,
+                         const void* u, const void* dw, uint64_t seed, int64_t traj_offset,
+                         int32_t sample_type, const void* dt, const void* coef, const void* G,
+                         void* y, void* disc, void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (num_steps < 1) return fail(DPAC_EINVAL, "num_steps must be >= 1");
+  if (td_type != DPAC_TD1 && td_type != DPAC_TD2) return fail(DPAC_EINVAL, "bad td_type %d", td_type);
+  if (cost_order != DPAC_COST_CRITIC && cost_order != DPAC_COST_ACTOR)
+    return fail(DPAC_EINVAL, "bad cost_order %d", cost_order);
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(u);
+  DPAC_REQUIRE(dt);
+  DPAC_REQUIRE(coef);
+  DPAC_REQUIRE(y);
+  DPAC_REQUIRE(disc);
+  if (td_type == DPAC_TD1) {
+    DPAC_REQUIRE(G);
+    if (!dw) {
+      if (int e = check_sample_type(sample_type)) return e;
+    }
+  }
+  OpArgs a = blank(eq, OP_TD_FWD);
+  a.td_type = td_type; a.cost_order = cost_order; a.dtype = dtype; a.B = num_sample;
+  a.N = num_steps; a.T = 1.0; a.x = x; a.u = u; a.dw = dw; a.seed = seed;
+  a.traj_offset = traj_offset;
+  a.sample_type = sample_type == DPAC_SAMPLE_ZERO_X0 ? DPAC_SAMPLE_NORMAL : sample_type;
+  a.dt_in = dt; a.coef_in = coef; a.G = G; a.y = y; a.disc = disc;
+  a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+int dpac_td_assemble_bwd(const dpac_eqn_params* eq, int32_t dtype, int64_t num_sample,
+                         int32_t num_steps, const void* x, const void* u, const void* dw,
+                         uint64_t seed, int64_t traj_offset, int32_t sample_type, const void* dt,
+                         const void* coef, const void* g_y, void* g_G, void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (num_steps < 1) return fail(DPAC_EINVAL, "num_steps must be >= 1");
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(u);
+  DPAC_REQUIRE(dt);
+  DPAC_REQUIRE(coef);
+  DPAC_REQUIRE(g_y);
+  DPAC_REQUIRE(g_G);
+  if (!dw) {
+    if (int e = check_sample_type(sample_type)) return e;
+  }
+  OpArgs a = blank(eq, OP_TD_BWD);
+  a.dtype = dtype; a.B = num_sample; a.N = num_steps; a.T = 1.0; a.x = x; a.u = u; a.dw = dw;
+  a.seed = seed; a.traj_offset = traj_offset;
+  a.sample_type = sample_type == DPAC_SAMPLE_ZERO_X0 ? DPAC_SAMPLE_NORMAL : sample_type;
+  a.dt_in = dt; a.coef_in = coef; a.g_y_out = g_y; a.g_G = g_G; a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype, int64_t num_sample,
+                        int32_t num_steps, const void* x, const void* u, const void* dt,
+                        const void* coef, void* y, void* disc, void* stream) {
+  return dpac_td_assemble_fwd(eq, DPAC_TD2, DPAC_COST_ACTOR, dtype, num_sample, num_steps, x, u,
+                              nullptr, 0, 0, DPAC_SAMPLE_NORMAL, dt, coef, nullptr, y, disc, stream);
+}
+
+int dpac_equation_eval(const dpac_eqn_params* eq, int32_t what, int32_t dtype, int64_t num_sample,
+                       const void* x, const void* u, void* out, void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (what < DPAC_EVAL_DRIFT || what > DPAC_EVAL_B) return fail(DPAC_EINVAL, "bad eval id %d", what);
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(out);
+  if ((what == DPAC_EVAL_DRIFT || what == DPAC_EVAL_SIGMA || what == DPAC_EVAL_W) && !u)
+    return fail(DPAC_EINVAL, "eval %d needs u", what);
+  OpArgs a = blank(eq, OP_EVAL);
+  a.what = what; a.dtype = dtype; a.B = num_sample; a.N = 1; a.T = 1.0; a.x = x; a.u = u;
+  a.out = out; a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+}  // extern "C"

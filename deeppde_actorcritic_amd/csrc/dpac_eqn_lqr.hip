@@ -1,0 +1,15 @@
+// Kernel instantiations for the LQR equation family (equation.py, class LQR),
+// compiled once per dtype: -DDPAC_TU_DOUBLE=0 (float) / 1 (double).
+#include "dpac_kernels.h"
+
+namespace dpac {
+template <typename T, int D>
+using EqLQRFor = EqLQR<T, D, lanes_for_dim(D)>;
+using lqrDims = DimList<EqLQRFor, DPAC_DIMS>;
+#if DPAC_TU_DOUBLE
+int dispatch_lqr_f64(const OpArgs& a) { return lqrDims::dispatch<double>(a); }
+#else
+int dispatch_lqr_f32(const OpArgs& a) { return lqrDims::dispatch<float>(a); }
+bool has_dim_lqr(int d) { return lqrDims::has(d); }
+#endif
+}  // namespace dpac

@@ -1,0 +1,259 @@
+"""Torch-facing wrappers of the libdpac C ABI (device-native layouts).
+
+Layouts (HBM, step-major): x0/x_bdry [B, d]; x [N+1, B, d]; dw, G [N, B, d];
+u [N, B, c]; dt, coef [N, B]; flags int32 [B]; y, disc [B].
+
+Every op requires CUDA (ROCm) tensors and raises if libdpac or the GPU is
+missing: there is no CPU path in the product.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import call
+
+_DT = {torch.float32: _lib.F32, torch.float64: _lib.F64}
+
+
+def _require_gpu(*tensors: torch.Tensor) -> None:
+    _lib.load()
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise _lib.DpacUnavailable(
+                "libdpac ops run on the GPU only; got a tensor on " f"{t.device}")
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("libdpac needs contiguous tensors")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _dtype_id(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"libdpac supports float32/float64, got {t.dtype}") from None
+
+
+def _check_same(ref: torch.Tensor, *others):
+    for o in others:
+        if o is not None and (o.dtype != ref.dtype or o.device != ref.device):
+            raise TypeError("all floating inputs must share dtype and device "
+                            f"({ref.dtype}@{ref.device} vs {o.dtype}@{o.device})")
+
+
+# ---------------------------------------------------------------------------
+def sample(eqp, sample_type: int, num_sample: int, num_steps: int, seed: int,
+           traj_offset: int = 0, dtype=torch.float32, device=None, want_dw=True):
+    """On-device Philox sampler (equation.py:13-44 semantics, different stream)."""
+    device = torch.device(device if device is not None else "cuda")
+    if device.type != "cuda":
+        raise _lib.DpacUnavailable("dpac_sample needs a GPU device")
+    _lib.load()
+    d = eqp.dim
+    x0 = torch.empty(num_sample, d, dtype=dtype, device=device)
+    x_bdry = torch.empty(num_sample, d, dtype=dtype, device=device)
+    dw = torch.empty(num_steps, num_sample, d, dtype=dtype, device=device) if want_dw else None
+    call("dpac_sample", ctypes.byref(eqp), sample_type, _DT[dtype], num_sample, num_steps,
+         seed & 0xFFFFFFFFFFFFFFFF, traj_offset, _ptr(x0), _ptr(dw), _ptr(x_bdry), _stream(x0))
+    return x0, dw, x_bdry
+
+
+def rollout_analytic(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor | None,
+                     total_time: float, num_steps: int, *, seed: int = 0,
+                     traj_offset: int = 0, sample_type: int = _lib.SAMPLE_NORMAL,
+                     want_u: bool = False, cost_order: int | None = None, out=None):
+    """Fused rollout with u = u_true (equation.py:46-106 with cheat=True).
+
+    Returns (x [N+1,B,d], dt [N,B], coef [N,B], u [N,B,c] | None, y [B] | None,
+    disc [B] | None).  dw=None draws increments in-kernel from the Philox stream.
+    """
+    _require_gpu(x0, dw)
+    _check_same(x0, dw)
+    B, d = x0.shape
+    N = num_steps
+    if dw is not None and tuple(dw.shape) != (N, B, d):
+        raise ValueError(f"dw must be [N, B, d] = {(N, B, d)}, got {tuple(dw.shape)}")
+    kw = dict(dtype=x0.dtype, device=x0.device)
+    if out is None:
+        x = torch.empty(N + 1, B, d, **kw)
+        dt = torch.empty(N, B, **kw)
+        coef = torch.empty(N, B, **kw)
+    else:
+        x, dt, coef = out
+    u = torch.empty(N, B, eqp.control_dim, **kw) if want_u else None
+    y = disc = None
+    if cost_order is not None:
+        y = torch.empty(B, **kw)
+        disc = torch.empty(B, **kw)
+    call("dpac_rollout_fwd", ctypes.byref(eqp), scheme, _dtype_id(x0), B, N, float(total_time),
+         _ptr(x0.contiguous()), _ptr(dw), seed & 0xFFFFFFFFFFFFFFFF, traj_offset, sample_type,
+         _ptr(x), _ptr(dt), _ptr(coef), _ptr(u), _lib.COST_CRITIC if cost_order is None
+         else cost_order, _ptr(y), _ptr(disc), _stream(x0))
+    return x, dt, coef, u, y, disc
+
+
+def flag_init(eqp, scheme: int, x0: torch.Tensor, total_time: float, num_steps: int):
+    _require_gpu(x0)
+    flag = torch.empty(x0.shape[0], dtype=torch.int32, device=x0.device)
+    call("dpac_flag_init", ctypes.byref(eqp), scheme, _dtype_id(x0), x0.shape[0], num_steps,
+         float(total_time), _ptr(x0.contiguous()), _ptr(flag), _stream(x0))
+    return flag
+
+
+class _SdeStep(torch.autograd.Function):
+    """One propagate-loop transition with an external control, fused with the
+    running cost/discount update; backward = dpac_step_bwd."""
+
+    @staticmethod
+    def forward(ctx, x, u, disc, y, dw_t, flag, eqp, scheme, T, N, cost_order):
+        B, d = x.shape
+        x_out = torch.empty_like(x)
+        disc_out = torch.empty_like(disc)
+        y_out = torch.empty_like(y)
+        dt = torch.empty_like(disc)
+        coef = torch.empty_like(disc)
+        flag_out = torch.empty_like(flag)
+        call("dpac_step_fwd", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
+             _ptr(x), _ptr(u), _ptr(dw_t), _ptr(flag), _ptr(disc), _ptr(y), cost_order,
+             _ptr(x_out), _ptr(flag_out), _ptr(disc_out), _ptr(y_out), _ptr(dt), _ptr(coef),
+             _stream(x))
+        ctx.save_for_backward(x, u, disc, dw_t, flag)
+        ctx.cfg = (eqp, scheme, T, N, cost_order)
+        ctx.mark_non_differentiable(dt, coef, flag_out)
+        return x_out, disc_out, y_out, dt, coef, flag_out
+
+    @staticmethod
+    def backward(ctx, g_x, g_disc, g_y, _gdt, _gcoef, _gflag):
+        x, u, disc, dw_t, flag = ctx.saved_tensors
+        eqp, scheme, T, N, cost_order = ctx.cfg
+        B = x.shape[0]
+        g_x = torch.zeros_like(x) if g_x is None else g_x.contiguous()
+        g_disc_c = None if g_disc is None else g_disc.contiguous()
+        g_y_c = None if g_y is None else g_y.contiguous()
+        gx = torch.empty_like(x)
+        gu = torch.empty_like(u)
+        gd = torch.empty_like(disc)
+        call("dpac_step_bwd", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T), _ptr(x),
+             _ptr(u), _ptr(dw_t), _ptr(flag), _ptr(disc), cost_order, _ptr(g_x), _ptr(g_disc_c),
+             _ptr(g_y_c), _ptr(gx), _ptr(gu), _ptr(gd), _stream(x))
+        if g_disc is None and g_y is None:
+            gd.zero_()
+        gy_in = g_y if g_y is not None else None
+        return gx, gu, gd, gy_in, None, None, None, None, None, None, None
+
+
+def sde_step(eqp, scheme: int, total_time: float, num_steps: int, x, u, dw_t, flag, disc, y,
+             cost_order: int = _lib.COST_ACTOR):
+    """x_{t+1}, disc_{t+1}, y_{t+1}, dt_t, coef_t, flag_{t+1} = step(x_t, u_t, ...)."""
+    _require_gpu(x, u, dw_t, disc, y)
+    _check_same(x, u, dw_t, disc, y)
+    return _SdeStep.apply(x.contiguous(), u.contiguous(), disc.contiguous(), y.contiguous(),
+                          dw_t.contiguous(), flag.contiguous(), eqp, scheme, total_time,
+                          num_steps, cost_order)
+
+
+class _TdAssemble(torch.autograd.Function):
+    """y, disc_N = TD target assembly (solver.py:166-187); grad flows to G only."""
+
+    @staticmethod
+    def forward(ctx, G, x, u, dw, dt, coef, eqp, td_type, cost_order, seed, traj_offset,
+                sample_type):
+        N, B = dt.shape
+        y = torch.empty(B, dtype=x.dtype, device=x.device)
+        disc = torch.empty_like(y)
+        call("dpac_td_assemble_fwd", ctypes.byref(eqp), td_type, cost_order, _dtype_id(x), B, N,
+             _ptr(x), _ptr(u), _ptr(dw), seed & 0xFFFFFFFFFFFFFFFF, traj_offset, sample_type,
+             _ptr(dt), _ptr(coef), _ptr(G), _ptr(y), _ptr(disc), _stream(x))
+        ctx.save_for_backward(x, u, dw, dt, coef)
+        ctx.cfg = (eqp, td_type, seed, traj_offset, sample_type, G is not None)
+        ctx.mark_non_differentiable(disc)
+        return y, disc
+
+    @staticmethod
+    def backward(ctx, g_y, _g_disc):
+        x, u, dw, dt, coef = ctx.saved_tensors
+        eqp, td_type, seed, traj_offset, sample_type, has_g = ctx.cfg
+        gG = None
+        if has_g and td_type == _lib.TD1 and g_y is not None and ctx.needs_input_grad[0]:
+            N, B = dt.shape
+            gG = torch.empty(N, B, eqp.dim, dtype=x.dtype, device=x.device)
+            call("dpac_td_assemble_bwd", ctypes.byref(eqp), _dtype_id(x), B, N, _ptr(x),
+                 _ptr(u), _ptr(dw), seed & 0xFFFFFFFFFFFFFFFF, traj_offset, sample_type,
+                 _ptr(dt), _ptr(coef), _ptr(g_y.contiguous()), _ptr(gG), _stream(x))
+        return gG, None, None, None, None, None, None, None, None, None, None, None
+
+
+def td_assemble(eqp, td_type: int, x, u, dw, dt, coef, G=None, *,
+                cost_order: int = _lib.COST_CRITIC, seed: int = 0, traj_offset: int = 0,
+                sample_type: int = _lib.SAMPLE_NORMAL):
+    """(y [B], disc_N [B]) over a finished trajectory; TD1 needs G [N,B,d]."""
+    _require_gpu(x, u, dw, dt, coef, G)
+    _check_same(x, u, dw, dt, coef, G)
+    if td_type == _lib.TD1 and G is None:
+        raise ValueError("TD1 needs G = NN_value_grad(x_t)")
+    G = None if (G is None or td_type != _lib.TD1) else G.contiguous()
+    return _TdAssemble.apply(G, x.contiguous(), u.contiguous(),
+                             None if dw is None else dw.contiguous(), dt.contiguous(),
+                             coef.contiguous(), eqp, td_type, cost_order, seed, traj_offset,
+                             sample_type)
+
+
+def actor_cost(eqp, x, u, dt, coef):
+    """Σ_t coef·w·dt·disc and disc_N over a finished trajectory (solver.py:213-219)."""
+    _require_gpu(x, u, dt, coef)
+    N, B = dt.shape
+    y = torch.empty(B, dtype=x.dtype, device=x.device)
+    disc = torch.empty_like(y)
+    call("dpac_actor_cost_fwd", ctypes.byref(eqp), _dtype_id(x), B, N, _ptr(x.contiguous()),
+         _ptr(u.contiguous()), _ptr(dt.contiguous()), _ptr(coef.contiguous()), _ptr(y),
+         _ptr(disc), _stream(x))
+    return y, disc
+
+
+def equation_eval(eqp, what: int, x: torch.Tensor, u: torch.Tensor | None = None):
+    """Row-wise Equation method on the device (equation.py:108-311)."""
+    _require_gpu(x, u)
+    _check_same(x, u)
+    x = x.contiguous()
+    B = x.shape[0]
+    if what in (_lib.EVAL_DRIFT, _lib.EVAL_SIGMA, _lib.EVAL_V_GRAD):
+        out = torch.empty(B, eqp.dim, dtype=x.dtype, device=x.device)
+    elif what == _lib.EVAL_U_TRUE:
+        out = torch.empty(B, eqp.control_dim, dtype=x.dtype, device=x.device)
+    else:
+        out = torch.empty(B, dtype=x.dtype, device=x.device)
+    call("dpac_equation_eval", ctypes.byref(eqp), what, _dtype_id(x), B, _ptr(x),
+         _ptr(None if u is None else u.contiguous()), _ptr(out), _stream(x))
+    return out
+
+
+class _VTrue(torch.autograd.Function):
+    """V_true(x) with gradient V_grad_true(x) (cheat_value path, solver.py:223)."""
+
+    @staticmethod
+    def forward(ctx, x, eqp):
+        ctx.save_for_backward(x)
+        ctx.eqp = eqp
+        return equation_eval(eqp, _lib.EVAL_V_TRUE, x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return g.unsqueeze(1) * equation_eval(ctx.eqp, _lib.EVAL_V_GRAD, x), None
+
+
+def v_true(eqp, x):
+    return _VTrue.apply(x, eqp)

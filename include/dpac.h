@@ -1,0 +1,224 @@
+/*
+ * dpac.h — C ABI of libdpac, the MI355X (gfx950) hot path of the actor-critic
+ * HJB solver: batched Euler–Maruyama rollout of the boundary-stopped controlled
+ * SDE, running-cost / discount accumulation, VR-LSTD (TD1) / LSTD (TD2) target
+ * assembly, the per-step transition used for back-propagation through the
+ * rollout, and the on-device Brownian sampler.
+ *
+ * The reference (MoZhou1995/DeepPDE_ActorCritic) has no FFI: its "plugin" surface
+ * is the Python `Equation` class in equation.py and the `CriticModel` /
+ * `ActorModel` classes in solver.py, with TensorFlow ops underneath.  Every entry
+ * point below replaces one of those Python/TF code paths; the replaced lines are
+ * cited on each declaration.  The Python package `deeppde_actorcritic_amd` binds
+ * this header with ctypes.
+ *
+ * Conventions
+ *  - Plain C: no C++ types, no torch types, no exceptions across the ABI.
+ *  - The caller owns every buffer.  All data pointers are DEVICE pointers
+ *    (hipMalloc / torch tensors on the GPU) unless the name says otherwise.
+ *  - Every launch is stream-ordered on `stream` (a hipStream_t; NULL = the legacy
+ *    default stream).  Nothing synchronises the host.
+ *  - `dtype` is DPAC_F32 or DPAC_F64 and applies to every floating buffer of the
+ *    call.  Flags are int32.
+ *  - Return value: 0 on success, DPAC_EINVAL for a bad argument, DPAC_EUNSUP for
+ *    an unsupported (equation, dim) combination, otherwise the hipError_t of the
+ *    failed launch.  dpac_last_error() returns a thread-local message.
+ *
+ * HBM layouts (step-major, one trajectory row per step; B = num_sample,
+ * d = dim, c = control_dim, N = num_steps):
+ *    x0, x_bdry  [B][d]            x     [N+1][B][d]      dw  [N][B][d]
+ *    u           [N][B][c]         dt    [N][B]           coef [N][B]
+ *    G           [N][B][d]         flag  [B] (int32)      y, disc [B]
+ * The reference keeps x_smp as [B][d][N+1], dw as [B][d][N] (equation.py:19,50,68);
+ * the Python shims transpose only at the parity boundary.
+ */
+#ifndef DPAC_H_
+#define DPAC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPAC_ABI_VERSION 1
+
+/* status codes besides hipError_t values */
+#define DPAC_OK 0
+#define DPAC_EINVAL (-1)
+#define DPAC_EUNSUP (-2)
+
+/* dtypes */
+#define DPAC_F32 0
+#define DPAC_F64 1
+
+/* equations — reference classes equation.py:144 (LQR), :179 (VDP), :240 (ekn), :278 (LQR_var) */
+#define DPAC_EQN_LQR 0
+#define DPAC_EQN_VDP 1
+#define DPAC_EQN_EKN 2
+#define DPAC_EQN_LQR_VAR 3
+
+/* time-stepping schemes — equation.py:46 (naive), :73 (adaptive) */
+#define DPAC_SCHEME_NAIVE 0
+#define DPAC_SCHEME_ADAPTIVE 1
+
+/* TD targets — solver.py:177 ("TD1" = VR-LSTD with the G control variate; "TD2" = LSTD) */
+#define DPAC_TD1 1
+#define DPAC_TD2 2
+
+/* cost-accumulation order: the critic (solver.py:170-174) and the actor
+ * (solver.py:218) multiply the same four factors in different orders */
+#define DPAC_COST_CRITIC 0
+#define DPAC_COST_ACTOR 1
+
+/* Brownian increments — equation.py:13 (normal), :25 (bounded 3-point), :38 (sample0) */
+#define DPAC_SAMPLE_NORMAL 0
+#define DPAC_SAMPLE_BOUNDED 1
+#define DPAC_SAMPLE_ZERO_X0 2 /* sample0: x0 = 0.01 in every component, dw normal */
+
+/* quantities for dpac_equation_eval (device versions of the Equation methods) */
+#define DPAC_EVAL_DRIFT 0     /* out [B][d]  equation.py:136 drift(x,u) */
+#define DPAC_EVAL_SIGMA 1     /* out [B][d]  diagonal of sigma(x,u), equation.py:132 */
+#define DPAC_EVAL_W 2         /* out [B]     w_tf(x,u), equation.py:108 */
+#define DPAC_EVAL_Z 3         /* out [B]     Z_tf(x), equation.py:112 */
+#define DPAC_EVAL_V_TRUE 4    /* out [B]     V_true(x), equation.py:124 */
+#define DPAC_EVAL_U_TRUE 5    /* out [B][c]  u_true(x), equation.py:128 */
+#define DPAC_EVAL_V_GRAD 6    /* out [B][d]  V_grad_true(x), e.g. equation.py:166 */
+#define DPAC_EVAL_B 7         /* out [B]     b_tf(x) = |x|^2 - R^2, equation.py:120 */
+
+/*
+ * Equation coefficients, filled by the host from eqn_config (equation.py:7-11 and
+ * each subclass __init__).  Derived constants are computed by the host exactly as
+ * the reference does: LQR k (equation.py:151), LQR_var k = (sqrt(5)-1)/2
+ * (equation.py:282), sigma_up = sqrt(2) (equation.py:152,186,247,286).
+ */
+typedef struct dpac_eqn_params {
+  int32_t eqn;         /* DPAC_EQN_* */
+  int32_t dim;         /* d */
+  int32_t control_dim; /* c (VDP: d/2, otherwise d) */
+  int32_t reserved;    /* must be 0 */
+  double gamma;        /* discount */
+  double R;            /* domain radius */
+  double sigma_up;     /* upper bound of sigma used by the adaptive scheme */
+  double p, q, beta, k; /* LQR (p,q,beta,k); LQR_var (q,beta,k); VDP (q) */
+  double a, epsilon;    /* VDP (a, epsilon); LQR_var (epsilon) */
+  double a2, a3;        /* EKN */
+} dpac_eqn_params;
+
+/* ---- introspection ------------------------------------------------------ */
+int32_t dpac_abi_version(void);
+const char* dpac_last_error(void);
+/* 1 if (eqn, dim, control_dim) has a compiled kernel instantiation */
+int32_t dpac_supported(const dpac_eqn_params* eq);
+
+/* ---- sampler (on-device, rocRAND Philox4x32-10) -------------------------
+ * Replaces Equation.sample_normal / sample_bounded / sample0
+ * (equation.py:13-23, 25-36, 38-44).  Trajectory b of this call is global
+ * trajectory traj_offset + b: the stream is keyed by (seed, global trajectory,
+ * step, component), so a batch sharded over ranks draws exactly the numbers the
+ * unsharded batch would.  Any of x0 / dw / x_bdry may be NULL to skip it. */
+int dpac_sample(const dpac_eqn_params* eq, int32_t sample_type, int32_t dtype,
+                int64_t num_sample, int32_t num_steps, uint64_t seed,
+                int64_t traj_offset, void* x0, void* dw, void* x_bdry,
+                void* stream);
+
+/* ---- fused rollout with the analytic control (the reference's `cheat` path)
+ * Replaces Equation.propagate_naive / propagate_adaptive with cheat=True
+ * (equation.py:46-71 / 73-106, control from u_true at :54-55 / :87-88).
+ * dw == NULL draws the increments in-kernel from the same Philox stream as
+ * dpac_sample(seed, traj_offset, sample_type).  u may be NULL (controls not kept).
+ * If cost != NULL the same launch also accumulates the running cost in the order
+ * cost_order and writes y[B] (Σ_t coef·w·dt·disc) and disc[B] (disc_N):
+ * the reference's ActorModel loop (solver.py:213-219) / the drift part of
+ * CriticModel (solver.py:166-175,187) under cheat_control. */
+int dpac_rollout_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                     int64_t num_sample, int32_t num_steps, double total_time,
+                     const void* x0, const void* dw, uint64_t seed,
+                     int64_t traj_offset, int32_t sample_type, void* x,
+                     void* dt, void* coef, void* u, int32_t cost_order,
+                     void* y, void* disc, void* stream);
+
+/* ---- one transition with an externally supplied control ----------------
+ * One iteration of the propagate loop body with u_t = NN_control(x_t) computed
+ * by the caller (equation.py:57-69 naive / :84-105 adaptive), fused with the
+ * actor's running-cost and discount update (solver.py:218-219, order
+ * DPAC_COST_ACTOR) or the critic's (solver.py:170-174,187, DPAC_COST_CRITIC).
+ * flag_in / flag_out are the scheme's per-trajectory flags (naive: 1 = alive,
+ * 0 = exited; adaptive: 2 inner, 1 boundary layer, 0 stopped); flag_out may alias
+ * flag_in.  y_in/y_out and disc_in/disc_out may alias.  Any of dt, coef may be
+ * NULL. */
+int dpac_flag_init(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                   int64_t num_sample, int32_t num_steps, double total_time,
+                   const void* x0, int32_t* flag, void* stream);
+
+int dpac_step_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                  int64_t num_sample, int32_t num_steps, double total_time,
+                  const void* x, const void* u, const void* dw_t,
+                  const int32_t* flag_in, const void* disc_in,
+                  const void* y_in, int32_t cost_order, void* x_out,
+                  int32_t* flag_out, void* disc_out, void* y_out, void* dt,
+                  void* coef, void* stream);
+
+/* Vector-Jacobian product of dpac_step_fwd for back-propagation through the
+ * rollout (what tf.GradientTape does for solver.py:95 through equation.py:84-105
+ * and solver.py:213-219).  Inputs are the SAME x, u, dw_t, flag_in, disc_in
+ * given to the forward call and the gradients of its outputs (g_x_out [B][d],
+ * g_disc_out [B], g_y_out [B]; g_disc_out / g_y_out may be NULL = zero).  Writes
+ * g_x [B][d], g_u [B][c], g_disc [B] (g_disc may be NULL).  The gradient of
+ * y_in is g_y_out (identity) and is not written.  Flags, coef and exit tests
+ * carry zero gradient, as TF's sign/floor/ceil do; the adaptive step size is
+ * differentiated through max(dt, 1e-4·Δt) with TF's tie rule. */
+int dpac_step_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                  int64_t num_sample, int32_t num_steps, double total_time,
+                  const void* x, const void* u, const void* dw_t,
+                  const int32_t* flag_in, const void* disc_in,
+                  int32_t cost_order, const void* g_x_out,
+                  const void* g_disc_out, const void* g_y_out, void* g_x,
+                  void* g_u, void* g_disc, void* stream);
+
+/* ---- TD target assembly ---------------------------------------------------
+ * The critic's per-step loop over a finished trajectory (solver.py:166-187):
+ *   y = Σ_t (w(x_t,u_t)·disc_t)·(coef_t·dt_t)
+ *       − [TD1] Σ_t (Σ_j (σ(x_t,u_t)dw_t)_j·G_j(x_t) · disc_t)·(coef_t·√dt_t)
+ *   disc_{t+1} = disc_t·exp(−γ·dt_t·coef_t),  disc_0 = 1
+ * Writes y[B] and disc[B] (= disc_N, the factor of V(x_N) in delta, solver.py:189).
+ * G may be NULL for TD2.  With td_type = DPAC_TD2 and cost_order = DPAC_COST_ACTOR
+ * this is the actor's pathwise cost without the terminal value
+ * (solver.py:213-219): dpac_actor_cost_fwd is that alias.
+ * dw may be NULL → regenerated from the Philox stream (seed, traj_offset,
+ * sample_type) exactly as dpac_sample / dpac_rollout_fwd drew it. */
+int dpac_td_assemble_fwd(const dpac_eqn_params* eq, int32_t td_type,
+                         int32_t cost_order, int32_t dtype, int64_t num_sample,
+                         int32_t num_steps, const void* x, const void* u,
+                         const void* dw, uint64_t seed, int64_t traj_offset,
+                         int32_t sample_type, const void* dt, const void* coef,
+                         const void* G, void* y, void* disc, void* stream);
+
+/* d y / d G for TD1: g_G[t][b][j] = −g_y[b]·disc_t·coef_t·√dt_t·(σ(x_t,u_t)dw_t)_j
+ * (the tape gradient of solver.py:177-184 with respect to NN_value_grad's output). */
+int dpac_td_assemble_bwd(const dpac_eqn_params* eq, int32_t dtype,
+                         int64_t num_sample, int32_t num_steps, const void* x,
+                         const void* u, const void* dw, uint64_t seed,
+                         int64_t traj_offset, int32_t sample_type,
+                         const void* dt, const void* coef, const void* g_y,
+                         void* g_G, void* stream);
+
+/* ActorModel pathwise cost without the terminal term (solver.py:213-219). */
+int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
+                        int64_t num_sample, int32_t num_steps, const void* x,
+                        const void* u, const void* dt, const void* coef,
+                        void* y, void* disc, void* stream);
+
+/* ---- device equation coefficients (for parity tests and metrics) -------
+ * Evaluates one Equation method row-wise on x [B][d] (and u [B][c] where the
+ * method takes a control): drift/sigma/w/Z/V_true/u_true/V_grad_true/b_tf
+ * (equation.py:108-311).  `what` is DPAC_EVAL_*. */
+int dpac_equation_eval(const dpac_eqn_params* eq, int32_t what, int32_t dtype,
+                       int64_t num_sample, const void* x, const void* u,
+                       void* out, void* stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* DPAC_H_ */

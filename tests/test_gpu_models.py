@@ -1,0 +1,115 @@
+"""GPU parity of the models and the training loop against the oracle (float64).
+
+The product (libdpac kernels + PyTorch MLPs on the GPU) and the oracle
+(torch-CPU restatement of solver.py/equation.py) start from the same weights and
+the same host-sampled inputs; losses and gradients must agree to 1e-9 relative
+(float64; the bound covers re-association inside GEMMs / reductions).
+"""
+import numpy as np
+import pytest
+import torch
+
+from deeppde_actorcritic_amd import equation as peq
+from deeppde_actorcritic_amd import solver as psol
+from oracle import equations as oeq
+from oracle import solver as osol
+from tests.helpers import full_config, rel_close
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+def pair(cfg, seed=0):
+    bp = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
+    bo = oeq.make(cfg.eqn_config)
+    sp = psol.ActorCriticSolver(cfg, bp, seed=seed, sampler="host")
+    params = {"critic": sp.model_critic.NN_value.export_params(),
+              "critic_grad": sp.model_critic.NN_value_grad.export_params(),
+              "actor": sp.model_actor.NN_control.export_params()}
+    so = osol.ActorCriticSolver(cfg, bo, params=params)
+    return sp, so
+
+
+def grads_close(gp, go, tol=TOL):
+    assert len(gp) == len(go)
+    for a, b in zip(gp, go):
+        if b is None:
+            assert a is None or float(a.abs().max()) == 0.0
+            continue
+        assert a is not None
+        assert rel_close(a.detach().cpu(), b.detach(), tol), float((a.detach().cpu() - b).abs().max())
+
+
+CASES = [("LQR", 5, "adaptive", "TD1"), ("LQR", 20, "naive", "TD2"), ("VDP", 4, "adaptive", "TD1"),
+         ("VDP", 10, "naive", "TD1"), ("EKN", 5, "adaptive", "TD1"), ("EKN", 5, "naive", "TD2"),
+         ("LQR_var", 5, "adaptive", "TD1"), ("LQR_var", 10, "naive", "TD1")]
+
+
+@pytest.mark.parametrize("name,d,scheme,td", CASES)
+def test_critic_loss_and_gradients(name, d, scheme, td):
+    cfg = full_config(name, d, N=12, batch=48, scheme=scheme, td=td)
+    sp, so = pair(cfg)
+    np.random.seed(4)
+    data = so.sample(48, 12)
+    for cheat in (False, True):
+        gp = sp.grad_critic(data, False, cheat)
+        go, lo = so.grad_critic(data, False, cheat)
+        lp = sp.loss_critic(data, False, cheat)
+        assert rel_close(float(lp), float(lo), TOL)
+        grads_close(gp, go)
+
+
+@pytest.mark.parametrize("name,d,scheme,td", CASES)
+def test_actor_loss_and_gradients(name, d, scheme, td):
+    """BPTT through the rollout: dpac_step_bwd + MLP autograd vs the oracle tape."""
+    cfg = full_config(name, d, N=12, batch=48, scheme=scheme, td=td)
+    sp, so = pair(cfg)
+    np.random.seed(5)
+    data = so.sample(48, 12)
+    for cheat_value in (False, True):
+        gp = sp.grad_actor(data, False, cheat_value, False)
+        go, lo = so.grad_actor(data, False, cheat_value, False)
+        lp = sp.loss_actor(data, False, cheat_value, False)
+        assert rel_close(float(lp), float(lo), TOL)
+        grads_close(gp, go)
+    with torch.no_grad():  # analytic control and value (true_loss_actor, solver.py:42)
+        lp = sp.loss_actor(data, False, True, True)
+    lo = so.loss_actor(data, False, True, True)
+    assert rel_close(float(lp), float(lo), TOL)
+
+
+@pytest.mark.parametrize("name,d,train", [("LQR", 5, "actor-critic"), ("VDP", 4, "critic"),
+                                          ("EKN", 5, "actor"), ("LQR_var", 5, "actor-critic")])
+def test_training_iterations_match_oracle(name, d, train):
+    """solver.py:36-71 end to end: same numpy stream, same weights, 3 iterations."""
+    cfg = full_config(name, d, N=8, batch=32, valid=32, iters=3, log_freq=1, train=train)
+    sp, so = pair(cfg, seed=11)
+    np.random.seed(123)
+    hp = sp.train()
+    np.random.seed(123)
+    ho = so.train()
+    assert hp[0].shape == ho.shape == (5, 9)
+    assert rel_close(hp[0][:, 1:8], ho[:, 1:8], 1e-8)
+    for vp, vo in zip(sp.critic_variables() + sp.actor_variables(),
+                      so.critic_vars() + so.actor_vars()):
+        assert rel_close(vp.detach().cpu(), vo.detach(), 1e-8)
+    x0, y, true_y, z, true_z, grad_y = hp[1:]
+    assert x0.shape == (32, d) and y.shape == (32, 1) and true_y.shape == (32, 1)
+    assert z.shape == true_z.shape == (32, cfg.eqn_config.control_dim) and grad_y.shape == (32, d)
+
+
+def test_reference_layout_propagate_surface():
+    """Equation.propagate_* keep the reference signature and layouts (equation.py:46, :73)."""
+    cfg = full_config("LQR", 5, N=10)
+    bp = peq.LQR(cfg.eqn_config)
+    bo = oeq.LQR(cfg.eqn_config)
+    np.random.seed(8)
+    x0, dw, _ = bo.sample_normal(16, 10)
+    from deeppde_actorcritic_amd.config import set_floatx
+    set_floatx("float64")
+    for name in ("propagate_naive", "propagate_adaptive"):
+        xs, dt, coef = getattr(bp, name)(16, x0, dw, None, False, 0.2, 10, True)
+        xr, dtr, cr = getattr(bo, name)(16, x0, dw, None, False, 0.2, 10, True)
+        assert tuple(xs.shape) == (16, 5, 11) and tuple(dt.shape) == (16, 10)
+        assert rel_close(xs.cpu(), xr, 1e-12) and rel_close(dt.cpu(), dtr, 1e-12)
+        assert np.array_equal(coef.cpu().numpy(), cr.numpy())
