@@ -10,7 +10,8 @@ OBJDIR    := build/obj
 DIMS      ?= 4,5,10,20
 DIMS_EVEN ?= 4,10,20
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
-             -DDPAC_DIMS=$(DIMS) -DDPAC_DIMS_EVEN=$(DIMS_EVEN) -Wno-pass-failed
+             -DDPAC_DIMS=$(DIMS) -DDPAC_DIMS_EVEN=$(DIMS_EVEN) -Wno-pass-failed \
+             -ffp-contract=off
 EQNS      := lqr lqrvar ekn vdp
 HDRS      := $(CSRC)/dpac_device.h $(CSRC)/dpac_kernels.h include/dpac.h
 OBJS      := $(OBJDIR)/dpac_abi.o \

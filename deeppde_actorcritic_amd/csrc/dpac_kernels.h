@@ -1,12 +1,17 @@
 // dpac_kernels.h — kernel templates of libdpac and the per-equation launcher.
 //
-// Mapping (all kernels): 64-thread workgroups = one wavefront; a trajectory is
-// owned by P = E::kP consecutive lanes, each holding M = d/P state components in
-// registers.  The time loop runs inside the kernel, so a trajectory's state
-// never leaves registers between steps; what goes to HBM is exactly what the
-// reference materialises (x_smp, dt, coef: equation.py:63-70, 97-104).
-// Per-step inputs (dw, and for the TD pass x/u/G/dt/coef) are prefetched
-// 2*KB steps ahead through a register ring (pipelined()).
+// Mapping: a trajectory is owned by P = E::kP consecutive lanes of a 64-wide
+// wavefront, each lane holding M = d/P state components in registers.
+//  * k_rollout: one wavefront per workgroup, the whole time loop in-kernel, so a
+//    trajectory's state never leaves registers between steps; HBM traffic is
+//    exactly what the reference materialises (x_smp, dt, coef: equation.py:63-70,
+//    97-104).  Per-step increments are prefetched 2*KB steps ahead (pipelined()).
+//  * k_td: the TD sums have no state dependence, only the discount product is
+//    sequential; 4 wavefronts per workgroup split the horizon into 4 chunks and
+//    combine (local sum, local discount) pairs in LDS.
+//  * k_step_fwd / k_step_bwd / k_flag_init / k_eval: one row per lane group.
+// Floating-point contraction is off (-ffp-contract=off); the fused multiply-adds
+// are written out, so every kernel variant rounds identically.
 #pragma once
 
 #include <cmath>
@@ -50,109 +55,129 @@ inline HostConsts host_consts(const OpArgs& a) {
   h.gamma = a.eq.gamma;
   h.R = a.eq.R;
   h.sigma_up = a.eq.sigma_up;
-  h.dt0 = a.T / a.N;                                          // delta_t = T / N (:48, :75)
-  h.sqrt_dt0 = std::sqrt(h.dt0);                              // np.sqrt(delta_t) (:49)
-  h.dt_min = h.dt0 * 1e-4;                                    // delta_t*1e-4 (:86)
-  h.den = 3 * a.eq.dim * (a.eq.sigma_up * a.eq.sigma_up);     // 3*dim*sigma_Up**2 (:85)
-  h.c_layer = a.eq.sigma_up * std::sqrt(3 * d * h.dt0);       // sigma_Up*sqrt(3*dim*dt) (:80, :94)
-  h.R2 = a.eq.R * a.eq.R;                                     // R**2 (:122)
+  h.dt0 = a.T / a.N;                                       // delta_t = T / N (:48, :75)
+  h.sqrt_dt0 = std::sqrt(h.dt0);                           // np.sqrt(delta_t) (:49)
+  h.dt_min = h.dt0 * 1e-4;                                 // delta_t*1e-4 (:86)
+  h.den = 3 * a.eq.dim * (a.eq.sigma_up * a.eq.sigma_up);  // 3*dim*sigma_Up**2 (:85)
+  h.c_layer = a.eq.sigma_up * std::sqrt(3 * d * h.dt0);    // sigma_Up*sqrt(3*dim*dt) (:80, :94)
+  h.R2 = a.eq.R * a.eq.R;                                  // R**2 (:122)
   return h;
 }
 
 template <typename T>
 struct DevConsts {
-  T gamma, R, dt0, sqrt_dt0, dt_min, den, c_layer, R2, neg_gamma;
+  T gamma, R, dt0, sqrt_dt0, dt_min, inv_den, two_inv_den, c_layer, R2, neg_gamma;
   static DevConsts make(const HostConsts& h) {
     DevConsts c;
     c.gamma = (T)h.gamma; c.R = (T)h.R; c.dt0 = (T)h.dt0; c.sqrt_dt0 = (T)h.sqrt_dt0;
-    c.dt_min = (T)h.dt_min; c.den = (T)h.den; c.c_layer = (T)h.c_layer; c.R2 = (T)h.R2;
-    c.neg_gamma = (T)(-h.gamma);
+    c.dt_min = (T)h.dt_min; c.inv_den = (T)(1.0 / h.den); c.two_inv_den = (T)(2.0 / h.den);
+    c.c_layer = (T)h.c_layer; c.R2 = (T)h.R2; c.neg_gamma = (T)(-h.gamma);
     return c;
   }
 };
 
+// sqrt: the hardware v_sqrt_f32 for float (1 ulp), correctly rounded for double.
+__device__ __forceinline__ float dsqrt(float v) { return __builtin_amdgcn_sqrtf(v); }
+__device__ __forceinline__ double dsqrt(double v) { return sqrt(v); }
+
 // ---------------------------------------------------------------------------
-// Software-pipelined time loop: frames for steps [t, t+KB) are loaded while
-// the previous KB steps compute.  Frame arrays are indexed only by unrolled
-// constants, so they live in VGPRs.
+// Software-pipelined time loop over [t_begin, t_end): frames for KB steps are
+// loaded while the previous KB steps compute.  Frame arrays are indexed only by
+// unrolled constants, so they live in VGPRs.
 // ---------------------------------------------------------------------------
 template <int KB, class F, class LoadF, class BodyF>
-__device__ __forceinline__ void pipelined(int N, LoadF&& load, BodyF&& body) {
+__device__ __forceinline__ void pipelined(int t_begin, int t_end, LoadF&& load, BodyF&& body) {
+  if (t_end <= t_begin) return;
+  const int last = t_end - 1;
   F A[KB], Bq[KB];
+  // Loads are never predicated: a load past the end re-reads the last step (in
+  // bounds, unused).  A predicated load would force its wait at the branch join
+  // and serialise the prefetch.
+#pragma unroll
+  for (int k = 0; k < KB; ++k) load(min(t_begin + k, last), A[k]);
+  int t0 = t_begin;
+  for (; t0 + 2 * KB <= t_end; t0 += 2 * KB) {
+#pragma unroll
+    for (int k = 0; k < KB; ++k) load(t0 + KB + k, Bq[k]);
+#pragma unroll
+    for (int k = 0; k < KB; ++k) body(t0 + k, A[k]);
+#pragma unroll
+    for (int k = 0; k < KB; ++k) load(min(t0 + 2 * KB + k, last), A[k]);
+#pragma unroll
+    for (int k = 0; k < KB; ++k) body(t0 + KB + k, Bq[k]);
+  }
+  // remainder (< 2*KB steps): A holds steps [t0, t0+KB)
 #pragma unroll
   for (int k = 0; k < KB; ++k)
-    if (k < N) load(k, A[k]);
-  for (int t0 = 0; t0 < N; t0 += 2 * KB) {
-#pragma unroll
-    for (int k = 0; k < KB; ++k)
-      if (t0 + KB + k < N) load(t0 + KB + k, Bq[k]);
-#pragma unroll
-    for (int k = 0; k < KB; ++k)
-      if (t0 + k < N) body(t0 + k, A[k]);
-#pragma unroll
-    for (int k = 0; k < KB; ++k)
-      if (t0 + 2 * KB + k < N) load(t0 + 2 * KB + k, A[k]);
-#pragma unroll
-    for (int k = 0; k < KB; ++k)
-      if (t0 + KB + k < N) body(t0 + KB + k, Bq[k]);
+    if (t0 + k < t_end) body(t0 + k, A[k]);
+  for (int t = t0 + KB; t < t_end; ++t) {
+    F f;
+    load(t, f);
+    body(t, f);
   }
 }
 
-// Lane coordinates: trajectory index b (clamped into range for the idle
-// groups of the last wave, which compute on a duplicate but never store) and
-// component slice p.
+// |v|^2 of the owned slice as a balanced tree (short dependency chain); every
+// kernel uses this one form so all variants round identically.
+template <typename T, int M>
+__device__ __forceinline__ T sumsq(const T (&v)[M]) {
+  T q[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) q[m] = v[m] * v[m];
+#pragma unroll
+  for (int w = 1; w < M; w *= 2) {
+#pragma unroll
+    for (int m = 0; m + w < M; m += 2 * w) q[m] = q[m] + q[m + w];
+  }
+  return q[0];
+}
+
+// Lane coordinates: trajectory b and component slice p.  Lane groups past the
+// end of the batch compute on a duplicate of the last trajectory and store the
+// same values it does (identical bits), so no store needs a divergent guard.
 template <int P>
 struct LaneCoord {
   int p;
   int64_t b;
   bool live;
-  __device__ LaneCoord(int64_t B) {
-    const int lane = threadIdx.x;
+  __device__ LaneCoord(int64_t B, int lane, int64_t group0) {
     p = lane % P;
-    b = (int64_t)blockIdx.x * (64 / P) + lane / P;
+    b = group0 + lane / P;
     live = b < B;
     if (!live) b = B - 1;
   }
 };
 
+// Adaptive flag of a point at radius r (equation.py:80-82, :94-95):
+// 1 + floor((sign(R-r-c) + sign(R-r))/2) = 2 if R-r-c > 0, 1 if R-r > 0, else 0.
 template <typename T>
-__device__ __forceinline__ int sgn(T v) {
-  return (v > T(0)) - (v < T(0));
+__device__ __forceinline__ int region_flag(T r, const DevConsts<T>& c) {
+  const T b = c.R - r;
+  return (b - c.c_layer > T(0)) ? 2 : (b > T(0) ? 1 : 0);
 }
 
-// floor(v/2) for v in {-2..2} (the reference's tf.math.floor(temp/2))
-__device__ __forceinline__ int floor_half(int v) { return v >= 0 ? v / 2 : -((-v + 1) / 2); }
-
-// Adaptive flag of a point at radius r: 2 inner, 1 boundary layer, 0 outside
-// (equation.py:80-82 and :94-95 before the sign(flag) factor).
-template <typename T>
-__device__ __forceinline__ int adaptive_flag(T r, const DevConsts<T>& c) {
-  const int tmp = sgn((c.R - r) - c.c_layer) + sgn(c.R - r);
-  return 1 + floor_half(tmp);
-}
-
-// Step size of the adaptive scheme (equation.py:85-86): (2f-f^2)(R-r)^2/den +
-// (f^2-2f+1)dt0 is exactly (R-r)^2/den for f == 1 and dt0 for f in {0, 2}.
+// (2f-f^2)(R-r)^2/den + (f^2-2f+1)dt0 (equation.py:85) is (R-r)^2/den for f == 1
+// and dt0 for f in {0, 2}; the division is a multiply by 1/den.
 template <typename T>
 __device__ __forceinline__ T adaptive_dt_raw(int flag, T r, const DevConsts<T>& c) {
-  return flag == 1 ? ((c.R - r) * (c.R - r)) / c.den : c.dt0;
+  const T b = c.R - r;
+  return flag == 1 ? (b * b) * c.inv_den : c.dt0;
 }
 
 // One transition of the scheme for the owned slice.  In: x, u, dw, flag, S = |x|^2.
-// Out: dx, coef, new flag, St = |x + dx|^2, dt and sqrt(dt).
+// Out: xt = x + dx, coef, new flag, St = |xt|^2, dt and sqrt(dt).
 template <typename T, class E, int SCHEME>
 struct Transition {
   static constexpr int M = E::M, MC = E::MC, P = E::kP;
-  T dx[M];
+  T xt[M], dx[M];
   T dt, sq, St;
   int coef, flag_new;
   __device__ __forceinline__ void run(const E& eq, const DevConsts<T>& c, const T (&x)[M],
                                       const T (&u)[MC], const T (&dw)[M], int flag, T S) {
     if constexpr (SCHEME == DPAC_SCHEME_ADAPTIVE) {
-      const T r = sqrt(S);
-      const T raw = adaptive_dt_raw(flag, r, c);
-      dt = raw >= c.dt_min ? raw : c.dt_min;  // tf.maximum(dt_i, delta_t*1e-4)
-      sq = sqrt(dt);
+      const T raw = adaptive_dt_raw(flag, dsqrt(S), c);
+      dt = raw >= c.dt_min ? raw : c.dt_min;  // tf.maximum(dt_i, delta_t*1e-4) (:86)
+      sq = dsqrt(dt);
     } else {
       dt = c.dt0;
       sq = c.sqrt_dt0;
@@ -160,37 +185,53 @@ struct Transition {
     T f[M], s[M];
     eq.drift(x, u, S, f);
     eq.sigma(x, u, s);
-    T acc = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      dx[m] = f[m] * dt + (s[m] * dw[m]) * sq;  // drift*dt + diffusion*sqrt(dt) (:58, :91)
-      const T xt = x[m] + dx[m];
-      acc += xt * xt;
+      dx[m] = fma(f[m], dt, (s[m] * dw[m]) * sq);  // drift*dt + diffusion*sqrt(dt) (:58, :91)
+      xt[m] = x[m] + dx[m];
     }
-    St = Lanes<P>::sum(acc);
+    St = Lanes<P>::sum(sumsq(xt));
     if constexpr (SCHEME == DPAC_SCHEME_ADAPTIVE) {
-      const int nf = flag > 0 ? adaptive_flag(sqrt(St), c) : 0;  // * sign(flag) (:95)
-      coef = (flag > 0 && nf > 0) ? 1 : 0;                          // sign(flag)*sign(new_flag) (:96)
-      flag_new = nf;
+      const int nf = region_flag(dsqrt(St), c);
+      flag_new = flag > 0 ? nf : 0;                  // * sign(flag) (:95)
+      coef = (flag > 0 && nf > 0) ? 1 : 0;          // sign(flag)*sign(new_flag) (:96)
     } else {
-      const int exit_ = (St - c.R2) >= T(0) ? 1 : 0;  // ceil((sign(b(x))+1)/2) (:60-61)
-      coef = flag * (1 - exit_);                      // (:62)
-      flag_new = coef;                                 // flag *= 1 - Exit (:69)
+      const bool out = St - c.R2 >= T(0);           // ceil((sign(b(x))+1)/2) == 1 (:60-61)
+      coef = (flag > 0 && !out) ? 1 : 0;            // flag*(1-Exit) (:62)
+      flag_new = coef;                               // flag *= 1 - Exit (:69)
     }
   }
 };
 
-template <typename T, int ORDER>
-__device__ __forceinline__ T cost_increment(T w, T coef, T dt, T disc) {
-  if constexpr (ORDER == DPAC_COST_ACTOR)
-    return ((coef * w) * dt) * disc;  // coef*w*dt*discount (solver.py:218)
-  else
-    return (w * disc) * (coef * dt);  // (w*discount)*(coef*dt) (solver.py:170-174)
+template <typename T>
+__device__ __forceinline__ T cost_increment(int order, T w, T coef, T dt, T disc) {
+  return order == DPAC_COST_ACTOR ? ((coef * w) * dt) * disc   // coef*w*dt*discount (solver.py:218)
+                                  : (w * disc) * (coef * dt);  // (w*discount)*(coef*dt) (:170-174)
 }
 
 template <typename T>
 __device__ __forceinline__ T disc_factor(T dt, T coef, const DevConsts<T>& c) {
   return exp((c.neg_gamma * dt) * coef);  // exp(-gamma*dt*coef) (solver.py:187, :219)
+}
+
+// Draw the increments of this lane's components for step t (in-kernel Philox).
+template <typename T, class E, int D>
+__device__ __forceinline__ void draw_owned(uint64_t seed, uint64_t gtraj, int t, int p, int sample_type,
+                                           T (&out)[E::M]) {
+  constexpr int P = E::kP, M = E::M;
+  if constexpr (P == 1) {
+    constexpr int R = lanes_for_dim(D), C = D / R;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      T tmp[C];
+      draw_chunk<T, D, C>(seed, gtraj, t, r, sample_type, tmp);
+#pragma unroll
+      for (int i = 0; i < C; ++i) out[r * C + i] = tmp[i];
+    }
+  } else {
+    static_assert(lanes_for_dim(D) == P, "RNG chunking follows the lane split");
+    draw_chunk<T, D, M>(seed, gtraj, t, p, sample_type, out);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -199,7 +240,7 @@ __device__ __forceinline__ T disc_factor(T dt, T coef, const DevConsts<T>& c) {
 template <typename T>
 struct RolloutArgs {
   int64_t B, traj_offset;
-  int N, sample_type;
+  int N, sample_type, cost_order;
   uint64_t seed;
   const T* x0;
   const T* dw;
@@ -211,45 +252,32 @@ struct DwFrame {
   T dw[M];
 };
 
-template <typename T, class E, int D, int SCHEME, bool PHILOX, bool COST, int ORDER, int KB>
+template <typename T, class E, int D, int SCHEME, bool PHILOX, bool COST, int KB>
 __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c,
                                                  const RolloutArgs<T> a) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
-  const LaneCoord<P> lc(a.B);
-  const int64_t B = a.B;
+  const LaneCoord<P> lc(a.B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
+  const int64_t stride = a.B * D;  // elements between consecutive steps of x / dw
   const int64_t row = lc.b * D + lc.p * M;
+  const T* __restrict__ dwp = a.dw + row;
+  T* __restrict__ xp = a.x + row;
+  // dt and coef leave in ONE store: lanes with p even write dt, odd write coef
+  T* __restrict__ dcp = (P == 1 ? a.dt : ((lc.p & 1) ? a.coef : a.dt)) + lc.b;
   T x[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) x[m] = a.x0[row + m];
-  if (lc.live) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) a.x[row + m] = x[m];
-  }
-  T acc = 0;
-#pragma unroll
-  for (int m = 0; m < M; ++m) acc += x[m] * x[m];
-  T S = Lanes<P>::sum(acc);
-  int flag = SCHEME == DPAC_SCHEME_ADAPTIVE ? adaptive_flag(sqrt(S), c) : 1;
+  for (int m = 0; m < M; ++m) xp[m] = x[m];
+  T S = Lanes<P>::sum(sumsq(x));
+  int flag = SCHEME == DPAC_SCHEME_ADAPTIVE ? region_flag(dsqrt(S), c) : 1;
   T disc = 1, y = 0;
   const uint64_t gtraj = (uint64_t)(a.traj_offset + lc.b);
 
   auto load = [&](int t, DwFrame<T, M>& fr) {
     if constexpr (PHILOX) {
-      if constexpr (P == 1) {
-        constexpr int R = lanes_for_dim(D), C = D / R;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          T tmp[C];
-          draw_chunk<T, D, C>(a.seed, gtraj, t, r, a.sample_type, tmp);
-#pragma unroll
-          for (int i = 0; i < C; ++i) fr.dw[r * C + i] = tmp[i];
-        }
-      } else {
-        static_assert(lanes_for_dim(D) == P, "RNG chunking follows the lane split");
-        draw_chunk<T, D, M>(a.seed, gtraj, t, lc.p, a.sample_type, fr.dw);
-      }
+      draw_owned<T, E, D>(a.seed, gtraj, t, lc.p, a.sample_type, fr.dw);
     } else {
-      const T* src = a.dw + ((int64_t)t * B) * D + row;
+      const T* src = dwp + t * stride;
 #pragma unroll
       for (int m = 0; m < M; ++m) fr.dw[m] = src[m];
     }
@@ -262,38 +290,32 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
     const T cf = (T)tr.coef;
     if constexpr (COST) {
       const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(x, u)));
-      y += cost_increment<T, ORDER>(w, cf, tr.dt, disc);
+      y += cost_increment(a.cost_order, w, cf, tr.dt, disc);
       disc = disc * disc_factor(tr.dt, cf, c);
     }
 #pragma unroll
-    for (int m = 0; m < M; ++m) x[m] = x[m] + tr.dx[m] * cf;  // x + delta_x*coef (:67, :103)
-    if (tr.coef) S = tr.St;
+    for (int m = 0; m < M; ++m) x[m] = tr.coef ? tr.xt[m] : x[m];  // x + delta_x*coef (:67, :103)
+    S = tr.coef ? tr.St : S;
     flag = tr.flag_new;
-    if (lc.live) {
-      T* xo = a.x + ((int64_t)(t + 1) * B) * D + row;
+    T* xo = xp + (t + 1) * stride;
 #pragma unroll
-      for (int m = 0; m < M; ++m) xo[m] = x[m];
-      if (a.u) {
-        T* uo = a.u + ((int64_t)t * B + lc.b) * (MC * P) + lc.p * MC;
+    for (int m = 0; m < M; ++m) xo[m] = x[m];
+    if (a.u) {
+      T* uo = a.u + ((int64_t)t * a.B + lc.b) * (MC * P) + lc.p * MC;
 #pragma unroll
-        for (int m = 0; m < MC; ++m) uo[m] = u[m];
-      }
-      const int64_t o = (int64_t)t * B + lc.b;
-      if constexpr (P == 1) {
-        a.dt[o] = tr.dt;
-        a.coef[o] = cf;
-      } else {
-        if (lc.p == 0) a.dt[o] = tr.dt;
-        if (lc.p == 1) a.coef[o] = cf;
-      }
+      for (int m = 0; m < MC; ++m) uo[m] = u[m];
+    }
+    if constexpr (P == 1) {
+      a.dt[(int64_t)t * a.B + lc.b] = tr.dt;
+      a.coef[(int64_t)t * a.B + lc.b] = cf;
+    } else {
+      dcp[(int64_t)t * a.B] = (lc.p & 1) ? cf : tr.dt;
     }
   };
-  pipelined<KB, DwFrame<T, M>>(a.N, load, body);
+  pipelined<KB, DwFrame<T, M>>(0, a.N, load, body);
   if constexpr (COST) {
-    if (lc.live && lc.p == 0) {
-      a.y[lc.b] = y;
-      a.disc[lc.b] = disc;
-    }
+    a.y[lc.b] = y;
+    a.disc[lc.b] = disc;
   }
 }
 
@@ -301,17 +323,16 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
 // Flag initialisation (adaptive: equation.py:78-82; naive: np.ones, :52)
 // ---------------------------------------------------------------------------
 template <typename T, class E, int D, int SCHEME>
-__global__ __launch_bounds__(64) void k_flag_init(const E eq, const DevConsts<T> c,
-                                                   int64_t B, const T* x0, int32_t* flag) {
+__global__ __launch_bounds__(64) void k_flag_init(const E eq, const DevConsts<T> c, int64_t B,
+                                                   const T* x0, int32_t* flag) {
   constexpr int P = E::kP, M = E::M;
-  const LaneCoord<P> lc(B);
+  const LaneCoord<P> lc(B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
   const int64_t row = lc.b * D + lc.p * M;
-  T acc = 0;
+  T xv[M];
 #pragma unroll
-  for (int m = 0; m < M; ++m) acc += x0[row + m] * x0[row + m];
-  const T S = Lanes<P>::sum(acc);
-  if (lc.live && lc.p == 0)
-    flag[lc.b] = SCHEME == DPAC_SCHEME_ADAPTIVE ? adaptive_flag(sqrt(S), c) : 1;
+  for (int m = 0; m < M; ++m) xv[m] = x0[row + m];
+  const T S = Lanes<P>::sum(sumsq(xv));
+  if (lc.p == 0) flag[lc.b] = SCHEME == DPAC_SCHEME_ADAPTIVE ? region_flag(dsqrt(S), c) : 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -320,6 +341,7 @@ __global__ __launch_bounds__(64) void k_flag_init(const E eq, const DevConsts<T>
 template <typename T>
 struct StepArgs {
   int64_t B;
+  int cost_order;
   const T *x, *u, *dw, *disc_in, *y_in;
   const int32_t* flag_in;
   T *x_out, *disc_out, *y_out, *dt, *coef;
@@ -329,36 +351,33 @@ struct StepArgs {
   T *g_x, *g_u, *g_disc;
 };
 
-template <typename T, class E, int D, int SCHEME, int ORDER>
+template <typename T, class E, int D, int SCHEME>
 __global__ __launch_bounds__(64) void k_step_fwd(const E eq, const DevConsts<T> c,
                                                   const StepArgs<T> a) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
-  const LaneCoord<P> lc(a.B);
+  const LaneCoord<P> lc(a.B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
   const int64_t row = lc.b * D + lc.p * M;
   const int64_t urow = lc.b * (MC * P) + lc.p * MC;
   T x[M], u[MC], dw[M];
-  T acc = 0;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     x[m] = a.x[row + m];
     dw[m] = a.dw[row + m];
-    acc += x[m] * x[m];
   }
 #pragma unroll
   for (int m = 0; m < MC; ++m) u[m] = a.u[urow + m];
-  const T S = Lanes<P>::sum(acc);
+  const T S = Lanes<P>::sum(sumsq(x));
   const int flag = a.flag_in[lc.b];
   const T disc = a.disc_in ? a.disc_in[lc.b] : T(1);
   Transition<T, E, SCHEME> tr;
   tr.run(eq, c, x, u, dw, flag, S);
   const T cf = (T)tr.coef;
   const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(x, u)));
-  if (!lc.live) return;  // after the last cross-lane op
 #pragma unroll
-  for (int m = 0; m < M; ++m) a.x_out[row + m] = x[m] + tr.dx[m] * cf;
+  for (int m = 0; m < M; ++m) a.x_out[row + m] = tr.coef ? tr.xt[m] : x[m];
   if (lc.p == 0) {
     const T yin = a.y_in ? a.y_in[lc.b] : T(0);
-    if (a.y_out) a.y_out[lc.b] = yin + cost_increment<T, ORDER>(w, cf, tr.dt, disc);
+    if (a.y_out) a.y_out[lc.b] = yin + cost_increment(a.cost_order, w, cf, tr.dt, disc);
     if (a.disc_out) a.disc_out[lc.b] = disc * disc_factor(tr.dt, cf, c);
     if (a.dt) a.dt[lc.b] = tr.dt;
     if (a.coef) a.coef[lc.b] = cf;
@@ -372,25 +391,23 @@ __global__ __launch_bounds__(64) void k_step_fwd(const E eq, const DevConsts<T> 
 //   dL/du    = c*dt*lam·∂f/∂u + c*sqrt(dt)*(lam⊙dw)·∂s/∂u + g_y'*c*dt*disc*∂w/∂u
 //   dL/dx    = lam + (same three terms w.r.t. x) + dL/ddt * ∂dt/∂x
 //   ∂dt/∂x   = -2(R-r)x/(r*den) if flag == 1 and dt_raw >= 1e-4 dt0 (TF max tie rule), else 0
-template <typename T, class E, int D, int SCHEME, int ORDER>
+template <typename T, class E, int D, int SCHEME>
 __global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> c,
                                                   const StepArgs<T> a) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
-  const LaneCoord<P> lc(a.B);
+  const LaneCoord<P> lc(a.B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
   const int64_t row = lc.b * D + lc.p * M;
   const int64_t urow = lc.b * (MC * P) + lc.p * MC;
   T x[M], u[MC], dw[M], lam[M];
-  T acc = 0;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     x[m] = a.x[row + m];
     dw[m] = a.dw[row + m];
     lam[m] = a.g_x_out[row + m];
-    acc += x[m] * x[m];
   }
 #pragma unroll
   for (int m = 0; m < MC; ++m) u[m] = a.u[urow + m];
-  const T S = Lanes<P>::sum(acc);
+  const T S = Lanes<P>::sum(sumsq(x));
   const int flag = a.flag_in[lc.b];
   const T disc = a.disc_in ? a.disc_in[lc.b] : T(1);
   const T gD1 = a.g_disc_out ? a.g_disc_out[lc.b] : T(0);
@@ -422,17 +439,15 @@ __global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> 
   eq.w_vjp(x, u, gw, gx, gu);
   const T g_disc = gD1 * Ef + gy1 * cf * w * tr.dt;
   if constexpr (SCHEME == DPAC_SCHEME_ADAPTIVE) {
-    const T g_dt = gD1 * disc * Ef * (c.neg_gamma * cf) + gy1 * cf * w * disc +
-                   cf * Lanes<P>::sum(part);
-    const T r = sqrt(S);
+    const T g_dt = gD1 * disc * Ef * (c.neg_gamma * cf) + gy1 * cf * w * disc + cf * Lanes<P>::sum(part);
+    const T r = dsqrt(S);
     const T raw = adaptive_dt_raw(flag, r, c);
     if (flag == 1 && raw >= c.dt_min) {
-      const T k = g_dt * (-2 * (c.R - r) / c.den) / r;
+      const T k = g_dt * (-(c.R - r) * c.two_inv_den) / r;
 #pragma unroll
       for (int m = 0; m < M; ++m) gx[m] += k * x[m];
     }
   }
-  if (!lc.live) return;
 #pragma unroll
   for (int m = 0; m < M; ++m) a.g_x[row + m] = gx[m];
 #pragma unroll
@@ -442,37 +457,47 @@ __global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> 
 
 // ---------------------------------------------------------------------------
 // TD target assembly over a finished trajectory (solver.py:166-190) and its
-// backward with respect to G.
+// backward with respect to G.  Workgroup = 4 wavefronts over the same 64/P
+// trajectories; wavefront w owns steps [w*Nc, (w+1)*Nc).  Each computes its
+// chunk with a local discount starting at 1, then the (sum, product) pairs are
+// combined in chunk order through LDS: y = Σ_w D_w L_w, D_{w+1} = D_w E_w.
 // ---------------------------------------------------------------------------
+constexpr int kTdChunks = 4;
+
 template <typename T>
 struct TdArgs {
   int64_t B, traj_offset;
-  int N, sample_type;
+  int N, sample_type, cost_order;
   uint64_t seed;
   const T *x, *u, *dw, *dt, *coef, *G, *g_y;
   T *y, *disc, *g_G;
 };
 
-template <typename T, int M, int MC, bool HAS_G>
+template <typename T, int M, int MC, bool HAS_DW, bool HAS_G>
 struct TdFrame {
-  T x[M], u[MC], dw[M], G[HAS_G ? M : 1];
+  T x[M], u[MC], dw[HAS_DW ? M : 1], G[HAS_G ? M : 1];
   T dt, coef;
 };
 
-template <typename T, class E, int D, bool TD1, bool PHILOX, int ORDER, bool BWD>
-__device__ __forceinline__ void td_common(const E& eq, const DevConsts<T>& c,
-                                          const TdArgs<T>& a) {
-  constexpr int P = E::kP, M = E::M, MC = E::MC;
+template <typename T, class E, int D, bool TD1, bool PHILOX, bool BWD>
+__global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, const TdArgs<T> a) {
+  constexpr int P = E::kP, M = E::M, MC = E::MC, GPW = 64 / P;
+  constexpr bool USE_DW = TD1 || BWD;
   constexpr bool HAS_G = TD1 && !BWD;
   constexpr int KB = sizeof(T) == 4 ? 4 : 2;
-  using F = TdFrame<T, M, MC, HAS_G>;
-  const LaneCoord<P> lc(a.B);
+  using F = TdFrame<T, M, MC, USE_DW && !PHILOX, HAS_G>;
+  __shared__ T s_sum[kTdChunks][GPW];
+  __shared__ T s_prod[kTdChunks][GPW];
+
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const LaneCoord<P> lc(a.B, lane, (int64_t)blockIdx.x * GPW);
+  const int g = lane / P;
   const int64_t B = a.B;
   const int64_t row = lc.b * D + lc.p * M;
   const int64_t urow = lc.b * (MC * P) + lc.p * MC;
   const uint64_t gtraj = (uint64_t)(a.traj_offset + lc.b);
-  T disc = 1, y = 0;
-  const T gy = BWD ? a.g_y[lc.b] : T(0);
+  const int nc = (a.N + kTdChunks - 1) / kTdChunks;
+  const int t_begin = min(a.N, wave * nc), t_end = min(a.N, (wave + 1) * nc);
 
   auto load = [&](int t, F& fr) {
     const int64_t so = (int64_t)t * B;
@@ -480,24 +505,9 @@ __device__ __forceinline__ void td_common(const E& eq, const DevConsts<T>& c,
     for (int m = 0; m < M; ++m) fr.x[m] = a.x[so * D + row + m];
 #pragma unroll
     for (int m = 0; m < MC; ++m) fr.u[m] = a.u[so * (MC * P) + urow + m];
-    if constexpr (TD1 || BWD) {
-      if constexpr (PHILOX) {
-        if constexpr (P == 1) {
-          constexpr int R = lanes_for_dim(D), C = D / R;
+    if constexpr (USE_DW && !PHILOX) {
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            T tmp[C];
-            draw_chunk<T, D, C>(a.seed, gtraj, t, r, a.sample_type, tmp);
-#pragma unroll
-            for (int i = 0; i < C; ++i) fr.dw[r * C + i] = tmp[i];
-          }
-        } else {
-          draw_chunk<T, D, M>(a.seed, gtraj, t, lc.p, a.sample_type, fr.dw);
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < M; ++m) fr.dw[m] = a.dw[so * D + row + m];
-      }
+      for (int m = 0; m < M; ++m) fr.dw[m] = a.dw[so * D + row + m];
     }
     if constexpr (HAS_G) {
 #pragma unroll
@@ -506,75 +516,93 @@ __device__ __forceinline__ void td_common(const E& eq, const DevConsts<T>& c,
     fr.dt = a.dt[so + lc.b];
     fr.coef = a.coef[so + lc.b];
   };
-  auto body = [&](int t, F& fr) {
-    if constexpr (!BWD) {
-      const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(fr.x, fr.u)));
-      y += cost_increment<T, ORDER>(w, fr.coef, fr.dt, disc);
-    }
-    if constexpr (TD1 || BWD) {
-      T s[M];
-      eq.sigma(fr.x, fr.u, s);
-      if constexpr (BWD) {
-        // d y / d G_j = -disc*coef*sqrt(dt)*diff_j ; g_G = g_y * that
-        const T k = -gy * (disc * (fr.coef * sqrt(fr.dt)));
-        if (lc.live) {
-          T* go = a.g_G + (int64_t)t * B * D + row;
+  auto increments = [&](int t, F& fr, T (&dwv)[M]) {
+    if constexpr (PHILOX) {
+      draw_owned<T, E, D>(a.seed, gtraj, t, lc.p, a.sample_type, dwv);
+    } else {
 #pragma unroll
-          for (int m = 0; m < M; ++m) go[m] = k * (s[m] * fr.dw[m]);
-        }
-      } else {
+      for (int m = 0; m < M; ++m) dwv[m] = fr.dw[m];
+    }
+  };
+
+  T disc = 1;
+  if constexpr (!BWD) {
+    T y = 0;
+    auto body = [&](int t, F& fr) {
+      const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(fr.x, fr.u)));
+      y += cost_increment(a.cost_order, w, fr.coef, fr.dt, disc);
+      if constexpr (TD1) {
+        T s[M], dwv[M];
+        eq.sigma(fr.x, fr.u, s);
+        increments(t, fr, dwv);
         T acc = 0;
 #pragma unroll
-        for (int m = 0; m < M; ++m) acc += (s[m] * fr.dw[m]) * fr.G[m];
+        for (int m = 0; m < M; ++m) acc = fma(s[m] * dwv[m], fr.G[m], acc);
         const T dot = Lanes<P>::sum(acc);
-        y -= (dot * disc) * (fr.coef * sqrt(fr.dt));  // solver.py:180-184
+        y -= (dot * disc) * (fr.coef * dsqrt(fr.dt));  // solver.py:180-184
       }
+      disc = disc * disc_factor(fr.dt, fr.coef, c);
+    };
+    pipelined<KB, F>(t_begin, t_end, load, body);
+    if (lc.p == 0) {
+      s_sum[wave][g] = y;
+      s_prod[wave][g] = disc;
     }
-    disc = disc * disc_factor(fr.dt, fr.coef, c);
-  };
-  pipelined<KB, F>(a.N, load, body);
-  if constexpr (!BWD) {
-    if (lc.live && lc.p == 0) {
-      a.y[lc.b] = y;
-      a.disc[lc.b] = disc;
+    __syncthreads();
+    if (wave == 0 && lc.p == 0) {
+      T Dw = 1, tot = 0;
+#pragma unroll
+      for (int w = 0; w < kTdChunks; ++w) {
+        tot += Dw * s_sum[w][g];
+        Dw *= s_prod[w][g];
+      }
+      a.y[lc.b] = tot;
+      a.disc[lc.b] = Dw;
     }
+  } else {
+    // pass A: the chunk's discount product from (dt, coef) only
+    for (int t = t_begin; t < t_end; ++t) {
+      const int64_t so = (int64_t)t * B + lc.b;
+      disc = disc * disc_factor(a.dt[so], a.coef[so], c);
+    }
+    if (lc.p == 0) s_prod[wave][g] = disc;
+    __syncthreads();
+    T Dw = 1;
+    for (int w = 0; w < wave; ++w) Dw *= s_prod[w][g];
+    disc = Dw;
+    const T gy = a.g_y[lc.b];
+    auto body = [&](int t, F& fr) {
+      T s[M], dwv[M];
+      eq.sigma(fr.x, fr.u, s);
+      increments(t, fr, dwv);
+      // d y / d G_j = -disc_t*coef_t*sqrt(dt_t)*diff_j
+      const T k = -gy * (disc * (fr.coef * dsqrt(fr.dt)));
+      T* go = a.g_G + (int64_t)t * B * D + row;
+#pragma unroll
+      for (int m = 0; m < M; ++m) go[m] = k * (s[m] * dwv[m]);
+      disc = disc * disc_factor(fr.dt, fr.coef, c);
+    };
+    pipelined<KB, F>(t_begin, t_end, load, body);
   }
 }
 
-template <typename T, class E, int D, bool TD1, bool PHILOX, int ORDER>
-__global__ __launch_bounds__(64) void k_td_fwd(const E eq, const DevConsts<T> c,
-                                                const TdArgs<T> a) {
-  td_common<T, E, D, TD1, PHILOX, ORDER, false>(eq, c, a);
-}
-
-template <typename T, class E, int D, bool PHILOX>
-__global__ __launch_bounds__(64) void k_td_bwd(const E eq, const DevConsts<T> c,
-                                                const TdArgs<T> a) {
-  td_common<T, E, D, true, PHILOX, DPAC_COST_CRITIC, true>(eq, c, a);
-}
-
 // ---------------------------------------------------------------------------
-// Row-wise evaluation of one Equation method (parity tests, metrics).  One row
-// per lane group as in every other kernel.
+// Row-wise evaluation of one Equation method (parity tests, metrics).
 // ---------------------------------------------------------------------------
 template <typename T, class E, int D>
 __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, int64_t B,
                                               int what, const T* x, const T* u, T* out) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
-  const LaneCoord<P> lc(B);
+  const LaneCoord<P> lc(B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
   const int64_t row = lc.b * D + lc.p * M;
   const int64_t urow = lc.b * (MC * P) + lc.p * MC;
   T xv[M], uv[MC];
-  T acc = 0;
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    xv[m] = x[row + m];
-    acc += xv[m] * xv[m];
-  }
+  for (int m = 0; m < M; ++m) xv[m] = x[row + m];
   const bool has_u = u != nullptr;
 #pragma unroll
   for (int m = 0; m < MC; ++m) uv[m] = has_u ? u[urow + m] : T(0);
-  const T S = Lanes<P>::sum(acc);
+  const T S = Lanes<P>::sum(sumsq(xv));
   T v[M];
   T scalar = 0;
   bool vec = false, ctl = false;
@@ -587,10 +615,8 @@ __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, i
     case DPAC_EVAL_U_TRUE: {
       T uu[MC];
       eq.u_true(xv, S, uu);
-      if (lc.live) {
 #pragma unroll
-        for (int m = 0; m < MC; ++m) out[urow + m] = uu[m];
-      }
+      for (int m = 0; m < MC; ++m) out[urow + m] = uu[m];
       ctl = true;
       break;
     }
@@ -598,7 +624,7 @@ __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, i
     case DPAC_EVAL_B: scalar = S - c.R2; break;
     default: break;
   }
-  if (!lc.live || ctl) return;
+  if (ctl) return;
   if (vec) {
 #pragma unroll
     for (int m = 0; m < M; ++m) out[row + m] = v[m];
@@ -623,28 +649,23 @@ int run_op(const OpArgs& a) {
   const dim3 grid = grid_for(a.B, P), block(64);
   hipStream_t s = a.stream;
   const bool adaptive = a.scheme == DPAC_SCHEME_ADAPTIVE;
-  const bool actor = a.cost_order == DPAC_COST_ACTOR;
   switch (a.op) {
     case OP_ROLLOUT: {
       RolloutArgs<T> r;
       r.B = a.B; r.traj_offset = a.traj_offset; r.N = a.N; r.sample_type = a.sample_type;
-      r.seed = a.seed;
+      r.cost_order = a.cost_order; r.seed = a.seed;
       r.x0 = (const T*)a.x0; r.dw = (const T*)a.dw;
       r.x = (T*)a.x_out; r.dt = (T*)a.dt; r.coef = (T*)a.coef; r.u = (T*)a.u_out;
       r.y = (T*)a.y; r.disc = (T*)a.disc;
       const bool philox = a.dw == nullptr, cost = a.y != nullptr;
       constexpr int KB = sizeof(T) == 4 ? 8 : 4;
-#define DPAC_ROLL(SCH, PH, CO, ORD) \
-  hipLaunchKernelGGL((k_rollout<T, E, D, SCH, PH, CO, ORD, KB>), grid, block, 0, s, eq, c, r)
-#define DPAC_ROLL_SCH(SCH)                                          \
-  if (philox) {                                                     \
-    if (!cost) DPAC_ROLL(SCH, true, false, 0);                      \
-    else if (actor) DPAC_ROLL(SCH, true, true, DPAC_COST_ACTOR);    \
-    else DPAC_ROLL(SCH, true, true, DPAC_COST_CRITIC);              \
-  } else {                                                          \
-    if (!cost) DPAC_ROLL(SCH, false, false, 0);                     \
-    else if (actor) DPAC_ROLL(SCH, false, true, DPAC_COST_ACTOR);   \
-    else DPAC_ROLL(SCH, false, true, DPAC_COST_CRITIC);             \
+#define DPAC_ROLL(SCH, PH, CO) \
+  hipLaunchKernelGGL((k_rollout<T, E, D, SCH, PH, CO, KB>), grid, block, 0, s, eq, c, r)
+#define DPAC_ROLL_SCH(SCH)                                                    \
+  if (philox) {                                                               \
+    if (cost) DPAC_ROLL(SCH, true, true); else DPAC_ROLL(SCH, true, false);   \
+  } else {                                                                    \
+    if (cost) DPAC_ROLL(SCH, false, true); else DPAC_ROLL(SCH, false, false); \
   }
       if (adaptive) { DPAC_ROLL_SCH(DPAC_SCHEME_ADAPTIVE) } else { DPAC_ROLL_SCH(DPAC_SCHEME_NAIVE) }
 #undef DPAC_ROLL_SCH
@@ -662,7 +683,7 @@ int run_op(const OpArgs& a) {
     case OP_STEP_FWD:
     case OP_STEP_BWD: {
       StepArgs<T> st;
-      st.B = a.B;
+      st.B = a.B; st.cost_order = a.cost_order;
       st.x = (const T*)a.x; st.u = (const T*)a.u; st.dw = (const T*)a.dw;
       st.disc_in = (const T*)a.disc_in; st.y_in = (const T*)a.y_in; st.flag_in = a.flag_in;
       st.x_out = (T*)a.x_out; st.disc_out = (T*)a.disc_out; st.y_out = (T*)a.y_out;
@@ -670,44 +691,35 @@ int run_op(const OpArgs& a) {
       st.g_x_out = (const T*)a.g_x_out; st.g_disc_out = (const T*)a.g_disc_out;
       st.g_y_out = (const T*)a.g_y_out;
       st.g_x = (T*)a.g_x; st.g_u = (T*)a.g_u; st.g_disc = (T*)a.g_disc;
-#define DPAC_STEP(K, SCH, ORD) hipLaunchKernelGGL((K<T, E, D, SCH, ORD>), grid, block, 0, s, eq, c, st)
-#define DPAC_STEP_K(K)                                                   \
-  if (adaptive) {                                                        \
-    if (actor) DPAC_STEP(K, DPAC_SCHEME_ADAPTIVE, DPAC_COST_ACTOR);      \
-    else DPAC_STEP(K, DPAC_SCHEME_ADAPTIVE, DPAC_COST_CRITIC);           \
-  } else {                                                               \
-    if (actor) DPAC_STEP(K, DPAC_SCHEME_NAIVE, DPAC_COST_ACTOR);         \
-    else DPAC_STEP(K, DPAC_SCHEME_NAIVE, DPAC_COST_CRITIC);              \
-  }
-      if (a.op == OP_STEP_FWD) { DPAC_STEP_K(k_step_fwd) } else { DPAC_STEP_K(k_step_bwd) }
-#undef DPAC_STEP_K
-#undef DPAC_STEP
+      if (a.op == OP_STEP_FWD) {
+        if (adaptive) hipLaunchKernelGGL((k_step_fwd<T, E, D, DPAC_SCHEME_ADAPTIVE>), grid, block, 0, s, eq, c, st);
+        else hipLaunchKernelGGL((k_step_fwd<T, E, D, DPAC_SCHEME_NAIVE>), grid, block, 0, s, eq, c, st);
+      } else {
+        if (adaptive) hipLaunchKernelGGL((k_step_bwd<T, E, D, DPAC_SCHEME_ADAPTIVE>), grid, block, 0, s, eq, c, st);
+        else hipLaunchKernelGGL((k_step_bwd<T, E, D, DPAC_SCHEME_NAIVE>), grid, block, 0, s, eq, c, st);
+      }
       break;
     }
     case OP_TD_FWD:
     case OP_TD_BWD: {
       TdArgs<T> td;
       td.B = a.B; td.traj_offset = a.traj_offset; td.N = a.N; td.sample_type = a.sample_type;
-      td.seed = a.seed;
+      td.cost_order = a.cost_order; td.seed = a.seed;
       td.x = (const T*)a.x; td.u = (const T*)a.u; td.dw = (const T*)a.dw;
       td.dt = (const T*)a.dt_in; td.coef = (const T*)a.coef_in; td.G = (const T*)a.G;
       td.g_y = (const T*)a.g_y_out;
       td.y = (T*)a.y; td.disc = (T*)a.disc; td.g_G = (T*)a.g_G;
       const bool philox = a.dw == nullptr;
+      const dim3 tblock(64 * kTdChunks);
+#define DPAC_TD(TD1, PH, BW) hipLaunchKernelGGL((k_td<T, E, D, TD1, PH, BW>), grid, tblock, 0, s, eq, c, td)
       if (a.op == OP_TD_BWD) {
-        if (philox) hipLaunchKernelGGL((k_td_bwd<T, E, D, true>), grid, block, 0, s, eq, c, td);
-        else hipLaunchKernelGGL((k_td_bwd<T, E, D, false>), grid, block, 0, s, eq, c, td);
+        if (philox) DPAC_TD(true, true, true); else DPAC_TD(true, false, true);
+      } else if (a.td_type == DPAC_TD1) {
+        if (philox) DPAC_TD(true, true, false); else DPAC_TD(true, false, false);
       } else {
-        const bool td1 = a.td_type == DPAC_TD1;
-#define DPAC_TD(TD1, PH, ORD) hipLaunchKernelGGL((k_td_fwd<T, E, D, TD1, PH, ORD>), grid, block, 0, s, eq, c, td)
-        if (td1) {
-          if (philox) { if (actor) DPAC_TD(true, true, DPAC_COST_ACTOR); else DPAC_TD(true, true, DPAC_COST_CRITIC); }
-          else { if (actor) DPAC_TD(true, false, DPAC_COST_ACTOR); else DPAC_TD(true, false, DPAC_COST_CRITIC); }
-        } else {
-          if (actor) DPAC_TD(false, false, DPAC_COST_ACTOR); else DPAC_TD(false, false, DPAC_COST_CRITIC);
-        }
-#undef DPAC_TD
+        DPAC_TD(false, false, false);
       }
+#undef DPAC_TD
       break;
     }
     case OP_EVAL:

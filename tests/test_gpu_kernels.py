@@ -171,7 +171,8 @@ def test_actor_cost_alias():
     x, dt, coef, u, y, disc = ops.rollout_analytic(eqp, 1, dev(x0), native_dw(dw), 0.2, 30, want_u=True,
                                                    cost_order=_lib.COST_ACTOR)
     y2, disc2 = ops.actor_cost(eqp, x, u, dt, coef)
-    assert torch.equal(y, y2) and torch.equal(disc, disc2)
+    # same sums; the TD kernel combines 4 horizon chunks, so only rounding differs
+    assert rel_close(y2.cpu(), y.cpu(), 1e-13) and rel_close(disc2.cpu(), disc.cpu(), 1e-13)
 
 
 # ---- sampler -------------------------------------------------------------------
@@ -264,9 +265,11 @@ def test_odd_batch_sizes():
     eo, ep = oeq.make(cfg), pe(cfg)
     for B in (1, 3, 17, 33):
         np.random.seed(B)
-        x0, dw, _ = eo.sample_normal(B, 12)
-        if B == 1:  # scipy squeezes size-1 axes
-            x0, dw = np.reshape(x0, (1, 20)), np.reshape(dw, (1, 20, 12))
+        if B == 1:  # the reference sampler cannot draw B = 1 (scipy squeezes size-1 axes, quirk 9)
+            x0 = np.random.uniform(-0.2, 0.2, size=(1, 20))
+            dw = np.random.standard_normal((1, 20, 12))
+        else:
+            x0, dw, _ = eo.sample_normal(B, 12)
         xr, dtr, cr = eo.propagate_adaptive(B, x0, dw, None, False, 0.2, 12, True)
         x, dt, coef, *_ = ops.rollout_analytic(ep.params(), 1, dev(x0), native_dw(dw), 0.2, 12)
         np.testing.assert_array_equal(coef.t().cpu().numpy(), cr.numpy())

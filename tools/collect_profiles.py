@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Copy rocprofv3 summaries from gpurun_out/ into profiles/ and derive HBM traffic.
+
+    python tools/collect_profiles.py r01
+
+* profiles/<tag>_kernel_stats.csv  — rocprofv3 --kernel-trace --stats summary
+* profiles/<tag>_pmc_rollout.json  — FETCH_SIZE / WRITE_SIZE per dpac::k_rollout launch,
+  corrected as MI355X_MICROARCH.md §HBM prescribes (separate passes; counters in KiB;
+  gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream -> x2)
+* profiles/pmc_traffic.json        — the per-launch HBM bytes bench.py reports as
+  roofline.traffic for the matching workload key
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+
+
+def counter_mean(path, kernel_substr, counter):
+    rows = [r for r in csv.DictReader(open(path))
+            if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    return statistics.mean(float(r["Counter_Value"]) for r in rows), len(rows), rows[0] if rows else None
+
+
+def main(tag):
+    os.makedirs(PROF, exist_ok=True)
+    ks = os.path.join(OUT, "prof_kt", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    f = os.path.join(OUT, "pmc_fetch", "run_counter_collection.csv")
+    w = os.path.join(OUT, "pmc_write", "run_counter_collection.csv")
+    if not (os.path.exists(f) and os.path.exists(w)):
+        print("no PMC passes found")
+        return
+    key_kernel = "k_rollout<float, dpac::EqLQR<float, 20, 4>, 20, 1, false, false"
+    fetch_kib, nf, row = counter_mean(f, key_kernel, "FETCH_SIZE")
+    write_kib, nw, _ = counter_mean(w, key_kernel, "WRITE_SIZE")
+    fetch_b = fetch_kib * 1024 * 2  # gfx950: FETCH_SIZE counts 64 B per 128-B request
+    write_b = write_kib * 1024
+    B, N, d = 4096, 200, 20
+    algo = B * N * (2 * d + 2) * 4 + B * d * 4  # + x0 read and x[0] write are per launch too
+    summary = {
+        "kernel": row["Kernel_Name"], "launches_fetch": nf, "launches_write": nw,
+        "FETCH_SIZE_KiB": fetch_kib, "WRITE_SIZE_KiB": write_kib,
+        "hbm_read_bytes_corrected": fetch_b, "hbm_write_bytes": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "algorithmic_bytes_per_launch": algo,
+        "traffic_over_algorithmic": (fetch_b + write_b) / algo,
+        "vgpr": row["VGPR_Count"], "sgpr": row["SGPR_Count"], "grid": row["Grid_Size"],
+        "workgroup": row["Workgroup_Size"],
+        "correction": "FETCH_SIZE x2 (MI355X_MICROARCH.md §HBM), counters in KiB, separate --pmc passes",
+    }
+    json.dump(summary, open(os.path.join(PROF, f"{tag}_pmc_rollout.json"), "w"), indent=2)
+    json.dump({"rollout_adaptive_f32_B4096_N200_d20": {"hbm_bytes_per_launch": fetch_b + write_b,
+                                                        "source": f"profiles/{tag}_pmc_rollout.json"}},
+              open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=2)
+    print(json.dumps(summary, indent=2))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")

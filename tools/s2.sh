@@ -1,0 +1,8 @@
+source tools/gpu_steps.sh
+export TMPDIR=/tmp
+R=$PWD
+run 900 pytest_gpu python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider
+run 300 bench python bench.py --steps 200 --warmup 20
+run 300 prof_kt rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline
+run 300 pmc_fetch rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
+run 300 pmc_write rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
