@@ -7,7 +7,7 @@ One "step" = one launch of dpac_rollout_fwd over one batch: LQR (p=q=beta=gamma=
 d = c = 20, B = 4096 trajectories per GPU, N = 200 steps, T = 0.2, adaptive
 scheme, analytic control (the reference's propagate_adaptive with cheat=True,
 equation.py:73-106), increments dw already resident in HBM, writing x [N+1,B,d],
-dt [N,B] and coef [N,B] — the canonical rollout of SURVEY.md §8(d).
+dt [B,N] and coef [B,N] — the canonical rollout of SURVEY.md §8(d).
 Trajectories shard across ranks by global index (weak scaling, no collective on
 the data path).  Rank 0 prints ONE JSON line.
 """
@@ -144,8 +144,8 @@ def main():
     x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=1234, traj_offset=off, dtype=dtype,
                            device="cuda")
     x = torch.empty(N + 1, B, d, dtype=dtype, device="cuda")
-    dt = torch.empty(N, B, dtype=dtype, device="cuda")
-    coef = torch.empty(N, B, dtype=dtype, device="cuda")
+    dt = torch.empty(B, N, dtype=dtype, device="cuda")
+    coef = torch.empty(B, N, dtype=dtype, device="cuda")
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     P = ctypes.c_void_p
     fn = lib.dpac_rollout_fwd

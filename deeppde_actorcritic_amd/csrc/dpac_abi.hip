@@ -108,6 +108,14 @@ OpArgs blank(const dpac_eqn_params* eq, int op) {
 int launch(const OpArgs& a) {
   int r = DPAC_EUNSUP;
   const bool f64 = a.dtype == DPAC_F64;
+  // Kernels address each [N+1][B][d] / [N][B][c] / [B][N] array through one
+  // 32-bit buffer descriptor whose offsets >= 2^31 mean "out of range".
+  const int64_t esz = f64 ? 8 : 4;
+  const int64_t width = a.eq.dim > a.eq.control_dim ? a.eq.dim : a.eq.control_dim;
+  if (a.B * width * ((int64_t)a.N + 1) * esz >= ((int64_t)1 << 31))
+    return fail(DPAC_EINVAL, "batch too large for one launch: every [N+1][B][d] array must stay "
+                "below 2 GiB (B=%lld, N=%d, d=%d); split the batch over launches with "
+                "traj_offset", (long long)a.B, a.N, a.eq.dim);
   switch (a.eq.eqn) {
     case DPAC_EQN_LQR: r = f64 ? dispatch_lqr_f64(a) : dispatch_lqr_f32(a); break;
     case DPAC_EQN_VDP: r = f64 ? dispatch_vdp_f64(a) : dispatch_vdp_f32(a); break;
@@ -125,20 +133,21 @@ int launch(const OpArgs& a) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int N, int D, int sample_type,
                                                    uint64_t seed, int64_t traj_offset, T* dw) {
-  const int R = lanes_for_dim(D), C = D / R;
+  // one thread per (t, b, lane slot p, block): the stream layout of draw_slot()
+  const int P = lanes_for_dim(D), M = comps_per_lane(D);
   const int PB = sample_type == DPAC_SAMPLE_BOUNDED ? 4 : Rng<T>::kNormalPerBlock;
-  const int BPC = (C + PB - 1) / PB;
-  const int64_t per_row = (int64_t)R * BPC;  // counter blocks per (t, b)
+  const int BPL = (M + PB - 1) / PB;
+  const int64_t per_row = (int64_t)P * BPL;  // counter blocks per (t, b)
   const int64_t total = (int64_t)N * B * per_row;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t tb = i / per_row;
     const int rem = (int)(i - tb * per_row);
-    const int r = rem / BPC, blk = rem % BPC;
+    const int p = rem / BPL, blk = rem % BPL;
     const int t = (int)(tb / B);
     const int64_t b = tb - (int64_t)t * B;
     const uint64_t traj = (uint64_t)(traj_offset + b);
-    const uint64_t block = (kTagDw << 48) | ((uint64_t)t * per_row + (uint64_t)r * BPC + blk);
+    const uint64_t block = (kTagDw << 48) | (((uint64_t)t * P + p) * BPL + blk);
     const uint4 v = philox_block(seed, traj, block);
     T vals[4];
     if (sample_type == DPAC_SAMPLE_BOUNDED) {
@@ -150,11 +159,11 @@ __global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int N, int D, int 
 #pragma unroll
       for (int e = 0; e < Rng<T>::kNormalPerBlock; ++e) vals[e] = n[e];
     }
-    T* out = dw + tb * D + r * C;
+    T* out = dw + tb * D;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int j = blk * PB + e;
-      if (e < PB && j < C) out[j] = vals[e];
+      const int m = blk * PB + e, j = p * M + m;
+      if (e < PB && m < M && j < D) out[j] = vals[e];
     }
   }
 }
@@ -215,9 +224,9 @@ int sample_impl(const dpac_eqn_params* eq, int32_t sample_type, int64_t B, int32
                 uint64_t seed, int64_t off, void* x0, void* dw, void* x_bdry, hipStream_t s) {
   const int D = eq->dim;
   if (dw) {
-    const int R = lanes_for_dim(D), C = D / R;
+    const int P = lanes_for_dim(D), M = comps_per_lane(D);
     const int PB = sample_type == DPAC_SAMPLE_BOUNDED ? 4 : Rng<T>::kNormalPerBlock;
-    const int64_t total = (int64_t)N * B * R * ((C + PB - 1) / PB);
+    const int64_t total = (int64_t)N * B * P * ((M + PB - 1) / PB);
     const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
     const int st = sample_type == DPAC_SAMPLE_ZERO_X0 ? DPAC_SAMPLE_NORMAL : sample_type;
     hipLaunchKernelGGL(k_sample_dw<T>, dim3((unsigned)blocks), dim3(256), 0, s, B, N, D, st, seed,

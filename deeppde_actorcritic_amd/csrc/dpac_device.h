@@ -1,9 +1,11 @@
 // dpac_device.h — device building blocks shared by every libdpac kernel:
-//   * lane-group reductions (a trajectory is owned by P consecutive lanes of a
-//     64-wide wavefront; sums over its d components use DPP / ds_swizzle),
-//   * the Brownian-increment stream (rocRAND Philox4x32-10 + Box–Muller),
+//   * the lane ownership model: a trajectory is owned by P consecutive lanes of
+//     a 64-wide wavefront; lane p owns components j = p + m*P (m < M), so one
+//     wave instruction touches P consecutive floats of a trajectory row;
+//   * lane-group reductions over the P lanes (DPP only, no LDS);
+//   * the Brownian-increment stream (rocRAND Philox4x32-10 + Box–Muller);
 //   * the four equation families as device functors (coefficients, analytic
-//     solutions and the vector-Jacobian products needed by the rollout backward).
+//     solutions and the vector-Jacobian products the rollout backward needs).
 //
 // Reference: equation.py:5-311 (Equation, LQR, VDP, ekn, LQR_var).
 #pragma once
@@ -17,82 +19,262 @@
 namespace dpac {
 
 // ---------------------------------------------------------------------------
-// Lane-group reductions.  Group g of a wave = lanes [g*P, g*P+P); every lane of
-// the group ends with the same (bitwise) sum because each butterfly level adds
-// two operands in commutative order.
+// Lane split.  P lanes per trajectory, M = ceil(D/P) components per lane with
+// P = min(16, next_pow2(ceil(D/2))): at most 2 components per lane up to d = 32,
+// so the per-step instruction stream of a wave is short and B = 4096, d = 20
+// gives 1024 wavefronts — one per SIMD of the 256-CU chip.
 // ---------------------------------------------------------------------------
-template <int MASK>
-__device__ __forceinline__ int shfl_xor_i32(int v) {
-  static_assert(MASK > 0 && MASK < 32, "group reductions stay within 32 lanes");
-  if constexpr (MASK == 1) {
-    return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);  // quad_perm(1,0,3,2)
-  } else if constexpr (MASK == 2) {
-    return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm(2,3,0,1)
-  } else {
-    return __builtin_amdgcn_ds_swizzle(v, (MASK << 10) | 0x1F);  // bit-mode xor
+__host__ __device__ constexpr int pow2_at_least(int v) {
+  int p = 1;
+  while (p < v) p *= 2;
+  return p;
+}
+// Timing experiments only: DPAC_LANE_CAP / DPAC_LANE_COMPS change the split.
+#ifndef DPAC_LANE_CAP
+#define DPAC_LANE_CAP 16
+#endif
+#ifndef DPAC_LANE_COMPS
+#define DPAC_LANE_COMPS 2
+#endif
+__host__ __device__ constexpr int lanes_for_dim(int D) {
+  return pow2_at_least((D + DPAC_LANE_COMPS - 1) / DPAC_LANE_COMPS) < DPAC_LANE_CAP
+             ? pow2_at_least((D + DPAC_LANE_COMPS - 1) / DPAC_LANE_COMPS)
+             : DPAC_LANE_CAP;
+}
+__host__ __device__ constexpr int comps_per_lane(int D) {
+  return (D + lanes_for_dim(D) - 1) / lanes_for_dim(D);
+}
+
+// Ownership of one lane: the CONTIGUOUS components j = p*M + m (m < M), so a
+// lane moves one M-element vector per row and a group's lanes cover the row
+// [b*d, b*d + d) in order — one fully coalesced instruction per row slab.
+// Lanes (or, for odd d, single elements) past d own nothing: their loads read
+// zero and their stores are dropped (buffer descriptors, see BufSlab), and every
+// componentwise equation maps zero components to zero contributions.
+template <int D, int P>
+struct Own {
+  static constexpr int M = (D + P - 1) / P;
+  static constexpr bool kFull = (D % M) == 0;  // every lane is either full or empty
+  int p;
+  __device__ explicit Own(int p_) : p(p_) {}
+  __device__ int j(int m) const { return p * M + m; }
+  __device__ bool valid(int m) const { return p * M + m < D; }
+  __device__ bool active() const { return p * M < D; }
+  template <typename T>
+  __device__ void mask(T (&v)[M]) const {
+#pragma unroll
+    for (int m = 0; m < M; ++m) v[m] = valid(m) ? v[m] : T(0);
+  }
+  // plain-pointer forms (predicated) for the single-step kernels
+  template <typename T>
+  __device__ void load_masked(const T* __restrict__ row, T (&v)[M]) const {
+#pragma unroll
+    for (int m = 0; m < M; ++m) v[m] = valid(m) ? row[p * M + m] : T(0);
+  }
+  template <typename T>
+  __device__ void store(T* __restrict__ row, const T (&v)[M]) const {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (valid(m)) row[p * M + m] = v[m];
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Buffer-descriptor access to [steps][rows][d] arrays (x / dw / u / G).  One
+// descriptor covers the whole array (num_records = its bytes, < 2 GiB — the
+// host checks); the per-lane voffset addresses the lane's elements inside one
+// step's slab and the wave-uniform soffset selects the step, so the time loop
+// spends one scalar add per array and step.  An out-of-range voffset (kOOB)
+// reads 0 and drops the store whether or not the hardware counts soffset in
+// the range check: inactive lanes and padding elements need no branch.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kOOB = 0x80000000u;
+constexpr int kRsrcFlags = 0x00020000;  // gfx950 raw-buffer descriptor word 3 (guide T8)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, kRsrcFlags);
+}
+
+template <int K>
+__device__ __forceinline__ void buf_load_dwords(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                                uint32_t (&w)[K], uint32_t soff = 0) {
+  constexpr int k4 = K / 4 * 4;
+#pragma unroll
+  for (int k = 0; k < k4; k += 4) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + 4 * k), (int)soff, 0);
+    w[k] = q[0]; w[k + 1] = q[1]; w[k + 2] = q[2]; w[k + 3] = q[3];
+  }
+  if constexpr (K - k4 == 3) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(voff + 4 * k4), (int)soff, 0);
+    w[k4] = q[0]; w[k4 + 1] = q[1]; w[k4 + 2] = q[2];
+  } else if constexpr (K - k4 == 2) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(voff + 4 * k4), (int)soff, 0);
+    w[k4] = q[0]; w[k4 + 1] = q[1];
+  } else if constexpr (K - k4 == 1) {
+    w[k4] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(voff + 4 * k4), (int)soff, 0);
   }
 }
 
-template <int MASK>
-__device__ __forceinline__ float shfl_xor(float v) {
-  return __builtin_bit_cast(float, shfl_xor_i32<MASK>(__builtin_bit_cast(int, v)));
+template <int K>
+__device__ __forceinline__ void buf_store_dwords(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                                 const uint32_t (&w)[K], uint32_t soff = 0) {
+  constexpr int k4 = K / 4 * 4;
+#pragma unroll
+  for (int k = 0; k < k4; k += 4) {
+    __attribute__((ext_vector_type(4))) unsigned int q = {w[k], w[k + 1], w[k + 2], w[k + 3]};
+    __builtin_amdgcn_raw_buffer_store_b128(q, r, (int)(voff + 4 * k), (int)soff, 0);
+  }
+  if constexpr (K - k4 == 3) {
+    __attribute__((ext_vector_type(3))) unsigned int q = {w[k4], w[k4 + 1], w[k4 + 2]};
+    __builtin_amdgcn_raw_buffer_store_b96(q, r, (int)(voff + 4 * k4), (int)soff, 0);
+  } else if constexpr (K - k4 == 2) {
+    __attribute__((ext_vector_type(2))) unsigned int q = {w[k4], w[k4 + 1]};
+    __builtin_amdgcn_raw_buffer_store_b64(q, r, (int)(voff + 4 * k4), (int)soff, 0);
+  } else if constexpr (K - k4 == 1) {
+    __builtin_amdgcn_raw_buffer_store_b32(w[k4], r, (int)(voff + 4 * k4), (int)soff, 0);
+  }
 }
-template <int MASK>
-__device__ __forceinline__ double shfl_xor(double v) {
+
+template <typename T>
+__device__ __forceinline__ void buf_store_scalar(__amdgpu_buffer_rsrc_t r, uint32_t voff, T v,
+                                                 uint32_t soff = 0) {
+  uint32_t w[sizeof(T) / 4];
+  __builtin_memcpy(&w[0], &v, sizeof(T));
+  buf_store_dwords<sizeof(T) / 4>(r, voff, w, soff);
+}
+
+// A lane's view of a [rows][D] slab: the byte offset of its M elements of row b
+// (kOOB when the lane owns nothing or the row is a padding duplicate).  Full
+// lanes move one vector; for odd D each element has its own offset.
+template <typename T, int D, int P>
+struct BufSlab {
+  static constexpr int M = Own<D, P>::M;
+  static constexpr bool kVec = Own<D, P>::kFull;
+  static constexpr int K = M * (int)sizeof(T) / 4;
+  uint32_t off[kVec ? 1 : M];
+  __device__ BufSlab(const Own<D, P>& own, int64_t b, bool live) {
+    if constexpr (kVec) {
+      off[0] = (live && own.active()) ? (uint32_t)((b * D + own.p * M) * (int64_t)sizeof(T)) : kOOB;
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        off[m] = (live && own.valid(m)) ? (uint32_t)((b * D + own.j(m)) * (int64_t)sizeof(T)) : kOOB;
+    }
+  }
+  // soff: wave-uniform byte offset of the row block (the step), in soffset.
+  __device__ void load(__amdgpu_buffer_rsrc_t r, T (&v)[M], uint32_t soff = 0) const {
+    if constexpr (kVec) {
+      uint32_t w[K];
+      buf_load_dwords<K>(r, off[0], w, soff);
+      __builtin_memcpy(&v[0], &w[0], sizeof(w));
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        uint32_t w[sizeof(T) / 4];
+        buf_load_dwords<sizeof(T) / 4>(r, off[m], w, soff);
+        __builtin_memcpy(&v[m], &w[0], sizeof(T));
+      }
+    }
+  }
+  __device__ void store(__amdgpu_buffer_rsrc_t r, const T (&v)[M], uint32_t soff = 0) const {
+    if constexpr (kVec) {
+      uint32_t w[K];
+      __builtin_memcpy(&w[0], &v[0], sizeof(w));
+      buf_store_dwords<K>(r, off[0], w, soff);
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        uint32_t w[sizeof(T) / 4];
+        __builtin_memcpy(&w[0], &v[m], sizeof(T));
+        buf_store_dwords<sizeof(T) / 4>(r, off[m], w, soff);
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Lane-group all-reduce over groups of P consecutive lanes, DPP only:
+// quad_perm xor1 / xor2, then row_half_mirror (8 lanes) and row_mirror (16).
+// Each level adds two operands in commutative order, so every lane of the
+// group ends with the same bits.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, dpp_i32<CTRL>(__builtin_bit_cast(int, v)));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
   const long long b = __builtin_bit_cast(long long, v);
-  const int lo = shfl_xor_i32<MASK>(static_cast<int>(b));
-  const int hi = shfl_xor_i32<MASK>(static_cast<int>(b >> 32));
-  return __builtin_bit_cast(
-      double, (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+  const int lo = dpp_i32<CTRL>(static_cast<int>(b));
+  const int hi = dpp_i32<CTRL>(static_cast<int>(b >> 32));
+  return __builtin_bit_cast(double,
+                            (static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+enum : int {
+  kDppXor1 = 0xB1,        // quad_perm(1,0,3,2)
+  kDppXor2 = 0x4E,        // quad_perm(2,3,0,1)
+  kDppHalfMirror = 0x141, // row_half_mirror: lane i <-> 7-i within 8
+  kDppMirror = 0x140,     // row_mirror: lane i <-> 15-i within 16
+};
+
+// Rows 2k and 2k+1 (16 lanes each) exchanged by v_permlane16_swap (gfx950):
+// the two results hold the even-row and the odd-row value in both rows.
+__device__ __forceinline__ float row_pair_sum(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto sw = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)sw[0]) + __builtin_bit_cast(float, (unsigned)sw[1]);
+}
+__device__ __forceinline__ double row_pair_sum(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  const auto sl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto sh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double a = __builtin_bit_cast(double, ((unsigned long long)(unsigned)sh[0] << 32) | (unsigned)sl[0]);
+  const double b = __builtin_bit_cast(double, ((unsigned long long)(unsigned)sh[1] << 32) | (unsigned)sl[1]);
+  return a + b;
 }
 
 template <int P>
 struct Lanes {
-  static_assert(P == 1 || P == 2 || P == 4 || P == 8 || P == 16, "bad group size");
+  static_assert(P == 1 || P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "bad group size");
   template <typename T>
   __device__ __forceinline__ static T sum(T v) {
-    if constexpr (P >= 2) v = v + shfl_xor<1>(v);
-    if constexpr (P >= 4) v = v + shfl_xor<2>(v);
-    if constexpr (P >= 8) v = v + shfl_xor<4>(v);
-    if constexpr (P >= 16) v = v + shfl_xor<8>(v);
+    if constexpr (P >= 2) v = v + dpp<kDppXor1>(v);
+    if constexpr (P >= 4) v = v + dpp<kDppXor2>(v);
+    if constexpr (P >= 8) v = v + dpp<kDppHalfMirror>(v);
+    if constexpr (P >= 16) v = v + dpp<kDppMirror>(v);
+    if constexpr (P >= 32) v = row_pair_sum(v);
     return v;
   }
 };
 
-// Lanes per trajectory for a componentwise equation of dimension D: keep ~4-5
-// components per lane so the per-trajectory scalar work (norms, step size,
-// flags) is shared by few lanes while B = 4096 still fills 256 CUs.
-__host__ __device__ constexpr int lanes_for_dim(int D) {
-  return (D % 4 == 0 && D >= 16) ? 4 : ((D % 2 == 0 && D >= 8) ? 2 : 1);
-}
-
 // ---------------------------------------------------------------------------
 // Brownian increments: rocRAND Philox4x32-10, subsequence = global trajectory
-// index, counter block = (tag << 48) | index.  The d components of step t are
-// cut into R = lanes_for_dim(d) chunks of C = d / R components; chunk r uses
-// BPC = ceil(C / PB) consecutive counter blocks, PB numbers per block (4 float
-// normals, 2 double normals, or 4 bounded values).  So a lane that owns one
-// chunk draws its own increments with no cross-lane traffic, and the stream is
-// a fixed function of (seed, global trajectory, t, j) for every GPU count.
+// index g, key = seed.  With P = lanes_for_dim(d), M = comps_per_lane(d),
+// component j = p*M + m of step t is element (m % PB) of counter block
+// (tag << 48) | ((t*P + p)*BPL + m / PB), BPL = ceil(M / PB), where PB numbers
+// come out of one block: 4 float normals, 2 double normals, or 4 bounded values.
+// A lane draws exactly the components it owns, and the stream is a fixed
+// function of (seed, g, t, j) for every GPU count and batch split.
 // Normal: rocRAND's Box–Muller (float: box_muller_hw below; double:
-// normal_distribution_double2).  Bounded:
-// k = floor(6·u32 / 2^32) ∈ {0..5}, value floor((k-1)/4)·√3 (equation.py:31-32).
+// normal_distribution_double2).  Bounded: k = floor(6·u32 / 2^32) ∈ {0..5},
+// value floor((k-1)/4)·√3 (equation.py:31-32).
 // ---------------------------------------------------------------------------
 enum : uint64_t { kTagDw = 0, kTagDir = 1, kTagRadius = 2, kTagBdry = 3 };
 
-__device__ __forceinline__ uint4 philox_block(uint64_t seed, uint64_t subseq,
-                                              uint64_t block) {
+__device__ __forceinline__ uint4 philox_block(uint64_t seed, uint64_t subseq, uint64_t block) {
   rocrand_state_philox4x32_10 st;
   rocrand_init(seed, subseq, block * 4ull, &st);
   return rocrand4(&st);  // the 4 words of counter `block`; the engine copy dies here
 }
 
-template <typename T>
-struct Rng;
 // rocRAND's float Box–Muller mapping (rocrand_normal.h box_muller: u in (0,1],
-// angle in (0, 2pi]) evaluated with the hardware v_log_f32 / v_sqrt_f32 /
-// v_sin/cos_f32 instead of the correctly-rounded expansions: ~1 ulp, ~4x fewer
-// instructions per normal.
+// angle in (0, 2pi]) with the hardware v_log_f32 / v_sqrt_f32 / v_sin,cos_f32
+// instead of the correctly-rounded expansions (~1 ulp).
 __device__ __forceinline__ void box_muller_hw(unsigned int x, unsigned int y, float& a, float& b) {
   const float u = ROCRAND_2POW32_INV + (x * ROCRAND_2POW32_INV);
   const float v = ROCRAND_2POW32_INV_2PI + (y * ROCRAND_2POW32_INV_2PI);
@@ -103,6 +285,8 @@ __device__ __forceinline__ void box_muller_hw(unsigned int x, unsigned int y, fl
   b = cs * s;
 }
 
+template <typename T>
+struct Rng;
 template <>
 struct Rng<float> {
   static constexpr int kNormalPerBlock = 4;
@@ -116,7 +300,8 @@ struct Rng<double> {
   static constexpr int kNormalPerBlock = 2;
   __device__ static void normals(uint4 v, double (&o)[2]) {
     const double2 n = rocrand_device::detail::normal_distribution_double2(v);
-    o[0] = n.x; o[1] = n.y;
+    o[0] = n.x;
+    o[1] = n.y;
   }
 };
 
@@ -132,43 +317,57 @@ __host__ __device__ constexpr int dw_per_block(int sample_type) {
   return sample_type == DPAC_SAMPLE_BOUNDED ? 4 : (sizeof(T) == 4 ? 4 : 2);
 }
 
-// Increments of chunk `r` (C components starting at r*C) of step t.
-template <typename T, int D, int C>
-__device__ __forceinline__ void draw_chunk(uint64_t seed, uint64_t traj, int t, int r,
-                                           int sample_type, T (&out)[C]) {
-  constexpr int R = D / C;
+// The M increments of lane slot p (components p*M + m) at step t.
+template <typename T, int D>
+__device__ __forceinline__ void draw_slot(uint64_t seed, uint64_t traj, int t, int p,
+                                          int sample_type, T (&out)[comps_per_lane(D)]) {
+  constexpr int P = lanes_for_dim(D), M = comps_per_lane(D);
   if (sample_type == DPAC_SAMPLE_BOUNDED) {
-    constexpr int BPC = (C + 3) / 4;
-    const uint64_t base = (uint64_t)t * (R * BPC) + (uint64_t)r * BPC;
+    constexpr int PB = 4, BPL = (M + PB - 1) / PB;
+    const uint64_t base = ((uint64_t)t * P + p) * BPL;
 #pragma unroll
-    for (int blk = 0; blk < BPC; ++blk) {
+    for (int blk = 0; blk < BPL; ++blk) {
       const uint4 v = philox_block(seed, traj, (kTagDw << 48) | (base + blk));
       const unsigned int w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (blk * 4 + e < C) out[blk * 4 + e] = bounded_value<T>(w[e]);
+      for (int e = 0; e < PB; ++e)
+        if (blk * PB + e < M) out[blk * PB + e] = bounded_value<T>(w[e]);
     }
   } else {
-    constexpr int PB = Rng<T>::kNormalPerBlock;
-    constexpr int BPC = (C + PB - 1) / PB;
-    const uint64_t base = (uint64_t)t * (R * BPC) + (uint64_t)r * BPC;
+    constexpr int PB = Rng<T>::kNormalPerBlock, BPL = (M + PB - 1) / PB;
+    const uint64_t base = ((uint64_t)t * P + p) * BPL;
 #pragma unroll
-    for (int blk = 0; blk < BPC; ++blk) {
+    for (int blk = 0; blk < BPL; ++blk) {
       T n[PB];
       Rng<T>::normals(philox_block(seed, traj, (kTagDw << 48) | (base + blk)), n);
 #pragma unroll
       for (int e = 0; e < PB; ++e)
-        if (blk * PB + e < C) out[blk * PB + e] = n[e];
+        if (blk * PB + e < M) out[blk * PB + e] = n[e];
     }
   }
 }
 
+// All D increments of step t in component order (for one-lane-per-trajectory kernels).
+template <typename T, int D>
+__device__ __forceinline__ void draw_all(uint64_t seed, uint64_t traj, int t, int sample_type,
+                                         T (&out)[D]) {
+  constexpr int P = lanes_for_dim(D), M = comps_per_lane(D);
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    T s[M];
+    draw_slot<T, D>(seed, traj, t, p, sample_type, s);
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (p * M + m < D) out[p * M + m] = s[m];
+  }
+}
+
 // ---------------------------------------------------------------------------
-// Equation functors.  A lane owns M = D/P consecutive state components
-// (j = p*M + m) and MC control components.  Methods see only the owned slice;
-// anything needing the whole vector receives the group-reduced |x|^2 (`S`) or
-// reduces through Lanes<P>.  All constants are computed on the host in double,
-// in the reference's evaluation order, then rounded to T.
+// Equation functors.  Methods see a lane's owned slice (M components, zero in
+// slots past d) and, where the equation needs it, the trajectory's norm r = |x|
+// (hot path) or both S = |x|^2 and r (analytic solutions).  Constants are
+// computed on the host in double, in the reference's evaluation order, then
+// rounded to T.
 // ---------------------------------------------------------------------------
 struct HostConsts {  // double-precision constants shared by all equations
   double gamma, R, sigma_up, dt0, sqrt_dt0, dt_min, den, c_layer, R2;
@@ -177,7 +376,7 @@ struct HostConsts {  // double-precision constants shared by all equations
 // LQR — equation.py:144-176
 template <typename T, int D, int P>
 struct EqLQR {
-  static constexpr int M = D / P, MC = M, kP = P;
+  static constexpr int M = (D + P - 1) / P, MC = M, kP = P, CDIM = D;
   static constexpr bool kNeedsNorm = false;
   T p, q, beta, kappa, two_kd, kR2, sqrt2, two_k, k, two_p, two_q;
   static EqLQR make(const dpac_eqn_params& e) {
@@ -210,22 +409,21 @@ struct EqLQR {
     return a;
   }
   __device__ T w_finish(T s) const { return s - two_kd; }
-  __device__ T V_true(const T (&x)[M], T S) const { return S * k; }
-  __device__ T Z(const T (&x)[M], T S) const { return kR2; }
-  __device__ void V_grad(const T (&x)[M], T S, T (&g)[M]) const {
+  __device__ T V_true(const T (&x)[M], T S, T r) const { return S * k; }
+  __device__ T Z(const T (&x)[M], T S, T r) const { return kR2; }
+  __device__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) g[m] = two_k * x[m];
   }
   // VJPs: accumulate a·∂drift/∂(x,u), a·∂sigma/∂(x,u), gw·∂w/∂(x,u)
-  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T S, const T (&a)[M],
+  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
                             T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) gu[m] += beta * a[m];
   }
-  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M],
-                            T (&gx)[M], T (&gu)[MC]) const {}
-  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M],
-                        T (&gu)[MC]) const {
+  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
+                            T (&gu)[MC]) const {}
+  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       gx[m] += gw * (two_p * x[m]);
@@ -237,10 +435,10 @@ struct EqLQR {
 // LQR_var — equation.py:278-311 (state- and control-dependent diagonal sigma)
 template <typename T, int D, int P>
 struct EqLQRVar {
-  static constexpr int M = D / P, MC = M, kP = P;
+  static constexpr int M = (D + P - 1) / P, MC = M, kP = P, CDIM = D;
   static constexpr bool kNeedsNorm = false;
-  T q, beta, eps, k, c1, c2, gk, two_kd, kR2, sqrt2, bpe, qk, e2, two_k, two_q, two_gk,
-      sqrt2_eps, two_c1q;
+  T q, beta, eps, k, c1, c2, gk, two_kd, kR2, sqrt2, bpe, qk, e2, two_k, two_q, two_gk, sqrt2_eps,
+      two_c1q;
   static EqLQRVar make(const dpac_eqn_params& e) {
     EqLQRVar r;
     r.q = (T)e.q; r.beta = (T)e.beta; r.eps = (T)e.epsilon; r.k = (T)e.k;
@@ -281,27 +479,26 @@ struct EqLQRVar {
     return a;
   }
   __device__ T w_finish(T s) const { return s - two_kd; }
-  __device__ T V_true(const T (&x)[M], T S) const { return S * k; }
-  __device__ T Z(const T (&x)[M], T S) const { return kR2; }
-  __device__ void V_grad(const T (&x)[M], T S, T (&g)[M]) const {
+  __device__ T V_true(const T (&x)[M], T S, T r) const { return S * k; }
+  __device__ T Z(const T (&x)[M], T S, T r) const { return kR2; }
+  __device__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) g[m] = two_k * x[m];
   }
-  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T S, const T (&a)[M],
+  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
                             T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) gu[m] += beta * a[m];
   }
-  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M],
-                            T (&gx)[M], T (&gu)[MC]) const {
+  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
+                            T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       gx[m] += a[m] * (sqrt2_eps * u[m]);
       gu[m] += a[m] * (sqrt2_eps * x[m]);
     }
   }
-  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M],
-                        T (&gu)[MC]) const {
+  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const T den = q + c2 * (x[m] * x[m]);
@@ -314,7 +511,7 @@ struct EqLQRVar {
 // ekn (configs say "EKN") — diffusive Eikonal, equation.py:240-276
 template <typename T, int D, int P>
 struct EqEKN {
-  static constexpr int M = D / P, MC = M, kP = P;
+  static constexpr int M = (D + P - 1) / P, MC = M, kP = P, CDIM = D;
   static constexpr bool kNeedsNorm = true;
   T a2, a3, K, two_a2, three_a3, sqrt2;
   static EqEKN make(const dpac_eqn_params& e) {
@@ -325,14 +522,12 @@ struct EqEKN {
     r.sqrt2 = (T)1.4142135623730951;
     return r;
   }
-  __device__ static T norm(T S) { return sqrt(S); }
-  __device__ void u_true(const T (&x)[M], T S, T (&u)[MC]) const {
-    const T r = norm(S);
+  __device__ void u_true(const T (&x)[M], T r, T (&u)[MC]) const {
 #pragma unroll
-    for (int m = 0; m < M; ++m) u[m] = x[m] / r;
+    for (int m = 0; m < M; ++m) u[m] = x[m] / r;  // x / |x| (:261)
   }
-  __device__ void drift(const T (&x)[M], const T (&u)[MC], T S, T (&f)[M]) const {
-    const T c = K / (two_a2 - three_a3 * norm(S));
+  __device__ void drift(const T (&x)[M], const T (&u)[MC], T r, T (&f)[M]) const {
+    const T c = K / (two_a2 - three_a3 * r);
 #pragma unroll
     for (int m = 0; m < M; ++m) f[m] = c * u[m];
   }
@@ -342,19 +537,15 @@ struct EqEKN {
   }
   __device__ T w_part(const T (&x)[M], const T (&u)[MC]) const { return 0; }
   __device__ T w_finish(T) const { return 1; }  // 0*sum(x) + 1 (:250)
-  __device__ T V_true(const T (&x)[M], T S) const {
-    const T r = norm(S);
-    return a3 * (r * r * r) - a2 * (r * r);
-  }
-  __device__ T Z(const T (&x)[M], T S) const { return V_true(x, S); }
-  __device__ void V_grad(const T (&x)[M], T S, T (&g)[M]) const {
-    const T c = three_a3 * norm(S) - two_a2;
+  __device__ T V_true(const T (&x)[M], T S, T r) const { return a3 * (r * r * r) - a2 * (r * r); }
+  __device__ T Z(const T (&x)[M], T S, T r) const { return V_true(x, S, r); }
+  __device__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
+    const T c = three_a3 * r - two_a2;
 #pragma unroll
     for (int m = 0; m < M; ++m) g[m] = c * x[m];
   }
-  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T S, const T (&a)[M],
+  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
                             T (&gx)[M], T (&gu)[MC]) const {
-    const T r = norm(S);
     const T den = two_a2 - three_a3 * r;
     const T c = K / den;
     T au = 0;
@@ -369,10 +560,9 @@ struct EqEKN {
 #pragma unroll
     for (int m = 0; m < M; ++m) gx[m] += f * x[m];
   }
-  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M],
-                            T (&gx)[M], T (&gu)[MC]) const {}
-  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M],
-                        T (&gu)[MC]) const {}
+  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
+                            T (&gu)[MC]) const {}
+  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {}
 };
 
 // VDP — stochastic Van der Pol oscillator, equation.py:179-238.  x = (x1, x2),
@@ -381,7 +571,7 @@ struct EqEKN {
 template <typename T, int D, int P>
 struct EqVDP {
   static_assert(P == 1 && D % 2 == 0, "VDP keeps a trajectory in one lane");
-  static constexpr int M = D, C = D / 2, MC = D / 2, kP = 1;
+  static constexpr int M = D, C = D / 2, MC = D / 2, kP = 1, CDIM = D / 2;
   static constexpr bool kNeedsNorm = false;
   T a, eps, q, gamma, geps, ga, two_ad, sqrt2, two_a, inv2q, two_ga, two_q;
   static EqVDP make(const dpac_eqn_params& e) {
@@ -438,18 +628,18 @@ struct EqVDP {
     return acc;
   }
   __device__ T w_finish(T s) const { return s - two_ad; }
-  __device__ T V_true(const T (&x)[M], T S) const {  // (:210)
+  __device__ T V_true(const T (&x)[M], T S, T r) const {  // (:210)
     T cross = 0;
 #pragma unroll
     for (int i = 0; i < C; ++i) cross += x[i] * x[nxt(i)] + x[C + i] * x[C + nxt(i)];
     return a * S - eps * cross;
   }
-  __device__ T Z(const T (&x)[M], T S) const { return V_true(x, S); }
-  __device__ void V_grad(const T (&x)[M], T S, T (&g)[M]) const {  // (:227)
+  __device__ T Z(const T (&x)[M], T S, T r) const { return V_true(x, S, r); }
+  __device__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {  // (:227)
     Lop(x, g);
     Lop(x + C, g + C);
   }
-  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T S, const T (&a)[M],
+  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
                             T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int i = 0; i < C; ++i) {
@@ -459,14 +649,13 @@ struct EqVDP {
       gu[i] += a2v;
     }
   }
-  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M],
-                            T (&gx)[M], T (&gu)[MC]) const {}
+  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
+                            T (&gu)[MC]) const {}
   // gradient of w (derivation in DESIGN.md §4.3): with L v = 2a v - eps(px v + nx v),
   // g = (1 - x1^2) x2 - x1:
   //   dw/dx1 = -gamma*eps*(px1+nx1) + 2 x1 x2 dv2 + 2 gamma a x1
   //   dw/dx2 = -gamma*eps*(px2+nx2) + L(dv2)/(2q) - dv1 - (1 - x1^2) dv2 - L(g) + 2 gamma a x2
-  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M],
-                        T (&gu)[MC]) const {
+  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
     T dv1[C], dv2[C], g[C], Ldv2[C], Lg[C];
     Lop(x, dv1);
     Lop(x + C, dv2);
@@ -479,8 +668,7 @@ struct EqVDP {
       const T x1 = x[i], x2 = x[C + i];
       const T s1 = x[nxt(i)] + x[prv(i)], s2 = x[C + nxt(i)] + x[C + prv(i)];
       const T d1 = geps * s1 + 2 * x1 * x2 * dv2[i] + two_ga * x1;
-      const T d2 = geps * s2 + Ldv2[i] * inv2q - dv1[i] - (1 - x1 * x1) * dv2[i] - Lg[i] +
-                   two_ga * x2;
+      const T d2 = geps * s2 + Ldv2[i] * inv2q - dv1[i] - (1 - x1 * x1) * dv2[i] - Lg[i] + two_ga * x2;
       gx[i] += gw * d1;
       gx[C + i] += gw * d2;
       gu[i] += gw * (two_q * u[i]);

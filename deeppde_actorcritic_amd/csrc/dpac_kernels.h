@@ -16,6 +16,7 @@
 
 #include <cmath>
 #include <type_traits>
+#include <utility>
 
 #include "dpac_device.h"
 
@@ -76,6 +77,26 @@ struct DevConsts {
   }
 };
 
+// Prefetch depth (steps per half ring) of the time loops.  The ring of 2*KB
+// frames gets a fixed VGPR budget, so wide per-lane frames (VDP keeps the whole
+// state in one lane) get a shallow ring instead of spilling: KB = 8 (f32) /
+// 4 (f64) for the canonical d = 20 rollout frame of 2 values.
+#ifndef DPAC_RING_VGPRS
+#define DPAC_RING_VGPRS 32
+#endif
+// KB = 0 (a frame larger than half the budget): no ring, each step loads its
+// own frame right before computing.
+constexpr int ring_kb(int frame_bytes, int budget_vgprs, int cap) {
+  const int kb = budget_vgprs * 4 / (2 * frame_bytes);
+  return kb > cap ? cap : kb;
+}
+// Timing-only ablations (never in a shipped build): 1 = skip the per-step
+// stores of x/dt/coef, 2 = synthesize dw instead of loading it, 3 = skip the
+// dt/coef stores, 4 = skip the x stores.
+#ifndef DPAC_ABLATE
+#define DPAC_ABLATE 0
+#endif
+
 // sqrt: the hardware v_sqrt_f32 for float (1 ulp), correctly rounded for double.
 __device__ __forceinline__ float dsqrt(float v) { return __builtin_amdgcn_sqrtf(v); }
 __device__ __forceinline__ double dsqrt(double v) { return sqrt(v); }
@@ -83,58 +104,83 @@ __device__ __forceinline__ double dsqrt(double v) { return sqrt(v); }
 // ---------------------------------------------------------------------------
 // Software-pipelined time loop over [t_begin, t_end): frames for KB steps are
 // loaded while the previous KB steps compute.  Frame arrays are indexed only by
-// unrolled constants, so they live in VGPRs.
+// unrolled constants, so they live in VGPRs.  body(t, frame, phase) receives
+// phase = (t - t_begin) mod 2*KB as a compile-time constant wherever the
+// unrolled position fixes it, and Phase<-1> in the scalar tail loop.
 // ---------------------------------------------------------------------------
+template <int V>
+using Phase = std::integral_constant<int, V>;
+
+// body(t + K, fr[K], Phase<BASE + K>) for K in the sequence; with CHECK,
+// bodies with t + K >= t_end are skipped.
+template <int BASE, bool CHECK, class F, class BodyF, int... K>
+__device__ __forceinline__ void run_bodies(BodyF& body, int t, F* fr, int t_end,
+                                           std::integer_sequence<int, K...>) {
+  if constexpr (CHECK)
+    ((t + K < t_end ? body(t + K, fr[K], Phase<BASE + K>{}) : void()), ...);
+  else
+    (body(t + K, fr[K], Phase<BASE + K>{}), ...);
+}
+
 template <int KB, class F, class LoadF, class BodyF>
 __device__ __forceinline__ void pipelined(int t_begin, int t_end, LoadF&& load, BodyF&& body) {
   if (t_end <= t_begin) return;
-  const int last = t_end - 1;
-  F A[KB], Bq[KB];
-  // Loads are never predicated: a load past the end re-reads the last step (in
-  // bounds, unused).  A predicated load would force its wait at the branch join
-  // and serialise the prefetch.
+  if constexpr (KB == 0) {
+    for (int t = t_begin; t < t_end; ++t) {
+      F f;
+      load(t, f);
+      body(t, f, Phase<-1>{});
+    }
+  } else {
+    const int last = t_end - 1;
+    F A[KB], Bq[KB];
+    // Loads are never predicated: a load past the end re-reads the last step (in
+    // bounds, unused).  A predicated load would force its wait at the branch join
+    // and serialise the prefetch.
 #pragma unroll
-  for (int k = 0; k < KB; ++k) load(min(t_begin + k, last), A[k]);
-  int t0 = t_begin;
-  for (; t0 + 2 * KB <= t_end; t0 += 2 * KB) {
+    for (int k = 0; k < KB; ++k) load(min(t_begin + k, last), A[k]);
+    int t0 = t_begin;
+    for (; t0 + 2 * KB <= t_end; t0 += 2 * KB) {
 #pragma unroll
-    for (int k = 0; k < KB; ++k) load(t0 + KB + k, Bq[k]);
+      for (int k = 0; k < KB; ++k) load(t0 + KB + k, Bq[k]);
+      run_bodies<0, false>(body, t0, A, t_end, std::make_integer_sequence<int, KB>{});
 #pragma unroll
-    for (int k = 0; k < KB; ++k) body(t0 + k, A[k]);
-#pragma unroll
-    for (int k = 0; k < KB; ++k) load(min(t0 + 2 * KB + k, last), A[k]);
-#pragma unroll
-    for (int k = 0; k < KB; ++k) body(t0 + KB + k, Bq[k]);
-  }
-  // remainder (< 2*KB steps): A holds steps [t0, t0+KB)
-#pragma unroll
-  for (int k = 0; k < KB; ++k)
-    if (t0 + k < t_end) body(t0 + k, A[k]);
-  for (int t = t0 + KB; t < t_end; ++t) {
-    F f;
-    load(t, f);
-    body(t, f);
+      for (int k = 0; k < KB; ++k) load(min(t0 + 2 * KB + k, last), A[k]);
+      run_bodies<KB, false>(body, t0 + KB, Bq, t_end, std::make_integer_sequence<int, KB>{});
+    }
+    // remainder (< 2*KB steps): A holds steps [t0, t0+KB)
+    run_bodies<0, true>(body, t0, A, t_end, std::make_integer_sequence<int, KB>{});
+    for (int t = t0 + KB; t < t_end; ++t) {
+      F f;
+      load(t, f);
+      body(t, f, Phase<-1>{});
+    }
   }
 }
 
-// |v|^2 of the owned slice as a balanced tree (short dependency chain); every
-// kernel uses this one form so all variants round identically.
+// |v|^2 of the owned slice (fma chain; every kernel uses this one form so all
+// variants round identically).
 template <typename T, int M>
 __device__ __forceinline__ T sumsq(const T (&v)[M]) {
-  T q[M];
+  T q = v[0] * v[0];
 #pragma unroll
-  for (int m = 0; m < M; ++m) q[m] = v[m] * v[m];
-#pragma unroll
-  for (int w = 1; w < M; w *= 2) {
-#pragma unroll
-    for (int m = 0; m + w < M; m += 2 * w) q[m] = q[m] + q[m + w];
-  }
-  return q[0];
+  for (int m = 1; m < M; ++m) q = fma(v[m], v[m], q);
+  return q;
 }
 
-// Lane coordinates: trajectory b and component slice p.  Lane groups past the
-// end of the batch compute on a duplicate of the last trajectory and store the
-// same values it does (identical bits), so no store needs a divergent guard.
+// XCD-aware block order (cdna_hip_programming.md §5.5 T1): the dispatcher deals
+// blocks round-robin over the 8 XCDs, so blocks b and b+1 — whose per-step rows
+// share cache lines (4 trajectories x 80 B = 2.5 lines) — would be written back
+// from two different L2s as partial lines.  Remap so that each XCD owns one
+// contiguous run of trajectory blocks (bijective for any grid size).
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// Lane coordinates: trajectory b and lane slot p within its group.  Lane groups
+// past the end of the batch compute on a duplicate of the last trajectory and
+// store the same values it does (identical bits), so no store needs a guard.
 template <int P>
 struct LaneCoord {
   int p;
@@ -148,42 +194,57 @@ struct LaneCoord {
   }
 };
 
-// Adaptive flag of a point at radius r (equation.py:80-82, :94-95):
-// 1 + floor((sign(R-r-c) + sign(R-r))/2) = 2 if R-r-c > 0, 1 if R-r > 0, else 0.
+// Adaptive-scheme state of a trajectory as two lane masks: alive = flag > 0,
+// layer = flag == 1 (equation.py:80-82: flag 2 inner, 1 boundary layer, 0 out).
+struct Flags {
+  bool alive, layer;
+  __device__ int encode() const { return alive ? (layer ? 1 : 2) : 0; }
+  __device__ static Flags decode(int f) { return Flags{f > 0, f == 1}; }
+};
+
+// Region of a point at radius r: 1 + floor((sign(R-r-c) + sign(R-r))/2) is
+// 2 if R-r-c > 0, 1 if R-r > 0, else 0 (equation.py:80-82, :94-95).
 template <typename T>
-__device__ __forceinline__ int region_flag(T r, const DevConsts<T>& c) {
+__device__ __forceinline__ Flags region(T r, const DevConsts<T>& c) {
   const T b = c.R - r;
-  return (b - c.c_layer > T(0)) ? 2 : (b > T(0) ? 1 : 0);
+  const bool inball = b > T(0);
+  const bool inner = b - c.c_layer > T(0);
+  return Flags{inball, inball && !inner};
 }
 
 // (2f-f^2)(R-r)^2/den + (f^2-2f+1)dt0 (equation.py:85) is (R-r)^2/den for f == 1
 // and dt0 for f in {0, 2}; the division is a multiply by 1/den.
 template <typename T>
-__device__ __forceinline__ T adaptive_dt_raw(int flag, T r, const DevConsts<T>& c) {
+__device__ __forceinline__ T adaptive_dt_raw(bool layer, T r, const DevConsts<T>& c) {
   const T b = c.R - r;
-  return flag == 1 ? (b * b) * c.inv_den : c.dt0;
+  return layer ? (b * b) * c.inv_den : c.dt0;
 }
 
-// One transition of the scheme for the owned slice.  In: x, u, dw, flag, S = |x|^2.
-// Out: xt = x + dx, coef, new flag, St = |xt|^2, dt and sqrt(dt).
+// One transition of the scheme for the owned slice.  In: x, u, dw (masked),
+// flags and r = |x|.  Out: xt = x + dx, coef, next flags, St = |xt|^2, rt = |xt|
+// (adaptive or norm-dependent equations), dt and sqrt(dt).
 template <typename T, class E, int SCHEME>
 struct Transition {
   static constexpr int M = E::M, MC = E::MC, P = E::kP;
+  static constexpr bool kRadius = SCHEME == DPAC_SCHEME_ADAPTIVE || E::kNeedsNorm;
   T xt[M], dx[M];
-  T dt, sq, St;
-  int coef, flag_new;
+  T dt, sq, St, rt;
+  bool coef;
+  Flags next;
   __device__ __forceinline__ void run(const E& eq, const DevConsts<T>& c, const T (&x)[M],
-                                      const T (&u)[MC], const T (&dw)[M], int flag, T S) {
+                                      const T (&u)[MC], const T (&dw)[M], Flags fl, T r) {
     if constexpr (SCHEME == DPAC_SCHEME_ADAPTIVE) {
-      const T raw = adaptive_dt_raw(flag, dsqrt(S), c);
-      dt = raw >= c.dt_min ? raw : c.dt_min;  // tf.maximum(dt_i, delta_t*1e-4) (:86)
+      // tf.maximum(dt_i, delta_t*1e-4) (:86): dt0 always exceeds the floor, so
+      // only the boundary-layer branch is clamped (same bits, one instruction less)
+      const T b = c.R - r;
+      dt = fl.layer ? fmax((b * b) * c.inv_den, c.dt_min) : c.dt0;
       sq = dsqrt(dt);
     } else {
       dt = c.dt0;
       sq = c.sqrt_dt0;
     }
     T f[M], s[M];
-    eq.drift(x, u, S, f);
+    eq.drift(x, u, r, f);
     eq.sigma(x, u, s);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -191,14 +252,15 @@ struct Transition {
       xt[m] = x[m] + dx[m];
     }
     St = Lanes<P>::sum(sumsq(xt));
+    rt = kRadius ? dsqrt(St) : T(0);
     if constexpr (SCHEME == DPAC_SCHEME_ADAPTIVE) {
-      const int nf = region_flag(dsqrt(St), c);
-      flag_new = flag > 0 ? nf : 0;                  // * sign(flag) (:95)
-      coef = (flag > 0 && nf > 0) ? 1 : 0;          // sign(flag)*sign(new_flag) (:96)
+      const Flags nf = region(rt, c);
+      coef = fl.alive && nf.alive;                 // sign(flag)*sign(new_flag) (:96)
+      next = Flags{coef, coef && nf.layer};        // new_flag*sign(flag) (:95)
     } else {
-      const bool out = St - c.R2 >= T(0);           // ceil((sign(b(x))+1)/2) == 1 (:60-61)
-      coef = (flag > 0 && !out) ? 1 : 0;            // flag*(1-Exit) (:62)
-      flag_new = coef;                               // flag *= 1 - Exit (:69)
+      const bool out = St - c.R2 >= T(0);         // ceil((sign(b(x))+1)/2) == 1 (:60-61)
+      coef = fl.alive && !out;                    // flag*(1-Exit) (:62)
+      next = Flags{coef, false};                  // flag *= 1 - Exit (:69)
     }
   }
 };
@@ -214,23 +276,16 @@ __device__ __forceinline__ T disc_factor(T dt, T coef, const DevConsts<T>& c) {
   return exp((c.neg_gamma * dt) * coef);  // exp(-gamma*dt*coef) (solver.py:187, :219)
 }
 
-// Draw the increments of this lane's components for step t (in-kernel Philox).
+// The increments of this lane's components at step t (in-kernel Philox).
 template <typename T, class E, int D>
-__device__ __forceinline__ void draw_owned(uint64_t seed, uint64_t gtraj, int t, int p, int sample_type,
-                                           T (&out)[E::M]) {
-  constexpr int P = E::kP, M = E::M;
-  if constexpr (P == 1) {
-    constexpr int R = lanes_for_dim(D), C = D / R;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      T tmp[C];
-      draw_chunk<T, D, C>(seed, gtraj, t, r, sample_type, tmp);
-#pragma unroll
-      for (int i = 0; i < C; ++i) out[r * C + i] = tmp[i];
-    }
+__device__ __forceinline__ void draw_owned(uint64_t seed, uint64_t gtraj, int t, int p,
+                                           int sample_type, T (&out)[E::M]) {
+  if constexpr (E::kP == 1) {
+    draw_all<T, D>(seed, gtraj, t, sample_type, out);
   } else {
-    static_assert(lanes_for_dim(D) == P, "RNG chunking follows the lane split");
-    draw_chunk<T, D, M>(seed, gtraj, t, p, sample_type, out);
+    static_assert(lanes_for_dim(D) == E::kP && comps_per_lane(D) == E::M,
+                  "RNG slots follow the lane split");
+    draw_slot<T, D>(seed, gtraj, t, p, sample_type, out);
   }
 }
 
@@ -252,42 +307,70 @@ struct DwFrame {
   T dw[M];
 };
 
-template <typename T, class E, int D, int SCHEME, bool PHILOX, bool COST, int KB>
+// Optional outputs of k_rollout (template bits, so the time loop never tests them).
+enum : int { kOutCost = 1, kOutU = 2 };
+
+template <typename T, class E, int D, int SCHEME, bool PHILOX, int OUT, int KB>
 __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c,
                                                  const RolloutArgs<T> a) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
-  const LaneCoord<P> lc(a.B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
-  const int64_t stride = a.B * D;  // elements between consecutive steps of x / dw
-  const int64_t row = lc.b * D + lc.p * M;
-  const T* __restrict__ dwp = a.dw + row;
-  T* __restrict__ xp = a.x + row;
-  // dt and coef leave in ONE store: lanes with p even write dt, odd write coef
-  T* __restrict__ dcp = (P == 1 ? a.dt : ((lc.p & 1) ? a.coef : a.dt)) + lc.b;
+  constexpr bool COST = (OUT & kOutCost) != 0, WANT_U = (OUT & kOutU) != 0;
+  // dt / coef rows are trajectory-major [B][N] (the reference's dt[B,N]): lane
+  // p of a group keeps step p of every F-step segment and the group writes the
+  // segment's F values of its row at once (F divides the pipeline period 2*KB,
+  // so each unrolled body knows its slot at compile time).
+  constexpr int F = P < 2 * KB ? P : 2 * KB;
+  using TR = Transition<T, E, SCHEME>;
+  const LaneCoord<P> lc(a.B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+  const Own<D, P> own(lc.p);
+  const Own<E::CDIM, P> ownu(lc.p);
+  const BufSlab<T, D, P> sx(own, lc.b, lc.live);           // x0, dw[t], x[t] rows
+  const BufSlab<T, E::CDIM, P> su(ownu, lc.b, lc.live);    // u[t] rows
+  // whole-array descriptors (host: every array < 2 GiB); the step goes in soffset
+  const uint32_t slab = (uint32_t)(a.B * D * sizeof(T));
+  const uint32_t slab_u = (uint32_t)(a.B * E::CDIM * sizeof(T));
+  const uint32_t row_bytes = (uint32_t)(a.N * sizeof(T));
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(a.x, slab * (uint32_t)(a.N + 1));
+  const __amdgpu_buffer_rsrc_t rs_dw = make_rsrc(a.dw, PHILOX ? 0u : slab * (uint32_t)a.N);
+  const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(a.u, WANT_U ? slab_u * (uint32_t)a.N : 0u);
+  const __amdgpu_buffer_rsrc_t rs_dt = make_rsrc(a.dt, (uint32_t)a.B * row_bytes);
+  const __amdgpu_buffer_rsrc_t rs_cf = make_rsrc(a.coef, (uint32_t)a.B * row_bytes);
+  const uint32_t off_row = lc.live ? (uint32_t)(lc.b * row_bytes + lc.p * sizeof(T)) : kOOB;
+  T dt_keep = 0, cf_keep = 0;
+  auto flush = [&](int seg, int count) {  // steps [seg, seg + count) of the row
+    const uint32_t off = lc.p < count ? off_row : kOOB;
+    buf_store_scalar<T>(rs_dt, off, dt_keep, (uint32_t)seg * (uint32_t)sizeof(T));
+    buf_store_scalar<T>(rs_cf, off, cf_keep, (uint32_t)seg * (uint32_t)sizeof(T));
+  };
+
   T x[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) x[m] = a.x0[row + m];
-#pragma unroll
-  for (int m = 0; m < M; ++m) xp[m] = x[m];
-  T S = Lanes<P>::sum(sumsq(x));
-  int flag = SCHEME == DPAC_SCHEME_ADAPTIVE ? region_flag(dsqrt(S), c) : 1;
+  sx.load(make_rsrc(a.x0, slab), x);
+  sx.store(rs_x, x);
+  T r = TR::kRadius ? dsqrt(Lanes<P>::sum(sumsq(x))) : T(0);
+  Flags fl = SCHEME == DPAC_SCHEME_ADAPTIVE ? region(r, c) : Flags{true, false};
   T disc = 1, y = 0;
   const uint64_t gtraj = (uint64_t)(a.traj_offset + lc.b);
 
   auto load = [&](int t, DwFrame<T, M>& fr) {
     if constexpr (PHILOX) {
       draw_owned<T, E, D>(a.seed, gtraj, t, lc.p, a.sample_type, fr.dw);
-    } else {
-      const T* src = dwp + t * stride;
+    } else if constexpr (DPAC_ABLATE == 2 || DPAC_ABLATE == 5) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) fr.dw[m] = src[m];
+      for (int m = 0; m < M; ++m) fr.dw[m] = T(((t * 7 + m + lc.p) & 3) - 1.5) * T(0.5);
+    } else {
+      sx.load(rs_dw, fr.dw, (uint32_t)t * slab);  // zero past d: no mask
     }
   };
-  auto body = [&](int t, DwFrame<T, M>& fr) {
+  auto body = [&](int t, DwFrame<T, M>& fr, auto phase) {
+    T dwv[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) dwv[m] = fr.dw[m];
+    if constexpr (PHILOX) own.mask(dwv);
     T u[MC];
-    eq.u_true(x, S, u);
-    Transition<T, E, SCHEME> tr;
-    tr.run(eq, c, x, u, fr.dw, flag, S);
-    const T cf = (T)tr.coef;
+    eq.u_true(x, r, u);
+    TR tr;
+    tr.run(eq, c, x, u, dwv, fl, r);
+    const T cf = tr.coef ? T(1) : T(0);
     if constexpr (COST) {
       const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(x, u)));
       y += cost_increment(a.cost_order, w, cf, tr.dt, disc);
@@ -295,27 +378,36 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) x[m] = tr.coef ? tr.xt[m] : x[m];  // x + delta_x*coef (:67, :103)
-    S = tr.coef ? tr.St : S;
-    flag = tr.flag_new;
-    T* xo = xp + (t + 1) * stride;
-#pragma unroll
-    for (int m = 0; m < M; ++m) xo[m] = x[m];
-    if (a.u) {
-      T* uo = a.u + ((int64_t)t * a.B + lc.b) * (MC * P) + lc.p * MC;
-#pragma unroll
-      for (int m = 0; m < MC; ++m) uo[m] = u[m];
+    if constexpr (TR::kRadius) r = tr.coef ? tr.rt : r;
+    fl = tr.next;
+    if constexpr (DPAC_ABLATE == 1 || DPAC_ABLATE == 5) {
+      if (t + 1 == a.N) sx.store(rs_x, x, (uint32_t)(t + 1) * slab);
+      return;
     }
-    if constexpr (P == 1) {
-      a.dt[(int64_t)t * a.B + lc.b] = tr.dt;
-      a.coef[(int64_t)t * a.B + lc.b] = cf;
-    } else {
-      dcp[(int64_t)t * a.B] = (lc.p & 1) ? cf : tr.dt;
+    if constexpr (DPAC_ABLATE != 4) sx.store(rs_x, x, (uint32_t)(t + 1) * slab);
+    if constexpr (WANT_U) su.store(rs_u, u, (uint32_t)t * slab_u);
+    if constexpr (DPAC_ABLATE != 3) {
+      constexpr int PH = decltype(phase)::value;
+      const int slot = PH >= 0 ? PH % F : (t & (F - 1));
+      dt_keep = lc.p == slot ? tr.dt : dt_keep;
+      cf_keep = lc.p == slot ? cf : cf_keep;
+      if constexpr (PH >= 0) {
+        if constexpr (PH % F == F - 1) flush(t - (F - 1), F);
+      } else if (slot == F - 1) {
+        flush(t - (F - 1), F);
+      }
     }
   };
   pipelined<KB, DwFrame<T, M>>(0, a.N, load, body);
+  if constexpr (DPAC_ABLATE != 3 && DPAC_ABLATE != 1 && DPAC_ABLATE != 5) {
+    const int rem = a.N & (F - 1);
+    if (rem) flush(a.N - rem, rem);
+  }
   if constexpr (COST) {
-    a.y[lc.b] = y;
-    a.disc[lc.b] = disc;
+    if (lc.live && lc.p == 0) {
+      a.y[lc.b] = y;
+      a.disc[lc.b] = disc;
+    }
   }
 }
 
@@ -326,13 +418,12 @@ template <typename T, class E, int D, int SCHEME>
 __global__ __launch_bounds__(64) void k_flag_init(const E eq, const DevConsts<T> c, int64_t B,
                                                    const T* x0, int32_t* flag) {
   constexpr int P = E::kP, M = E::M;
-  const LaneCoord<P> lc(B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
-  const int64_t row = lc.b * D + lc.p * M;
+  const LaneCoord<P> lc(B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+  const Own<D, P> own(lc.p);
   T xv[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) xv[m] = x0[row + m];
-  const T S = Lanes<P>::sum(sumsq(xv));
-  if (lc.p == 0) flag[lc.b] = SCHEME == DPAC_SCHEME_ADAPTIVE ? region_flag(dsqrt(S), c) : 1;
+  own.load_masked(x0 + lc.b * D, xv);
+  const T r = dsqrt(Lanes<P>::sum(sumsq(xv)));
+  if (lc.p == 0) flag[lc.b] = SCHEME == DPAC_SCHEME_ADAPTIVE ? region(r, c).encode() : 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -355,33 +446,32 @@ template <typename T, class E, int D, int SCHEME>
 __global__ __launch_bounds__(64) void k_step_fwd(const E eq, const DevConsts<T> c,
                                                   const StepArgs<T> a) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
-  const LaneCoord<P> lc(a.B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
-  const int64_t row = lc.b * D + lc.p * M;
-  const int64_t urow = lc.b * (MC * P) + lc.p * MC;
+  using TR = Transition<T, E, SCHEME>;
+  const LaneCoord<P> lc(a.B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+  const Own<D, P> own(lc.p);
+  const Own<E::CDIM, P> ownu(lc.p);
   T x[M], u[MC], dw[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    x[m] = a.x[row + m];
-    dw[m] = a.dw[row + m];
-  }
-#pragma unroll
-  for (int m = 0; m < MC; ++m) u[m] = a.u[urow + m];
-  const T S = Lanes<P>::sum(sumsq(x));
-  const int flag = a.flag_in[lc.b];
+  own.load_masked(a.x + lc.b * D, x);
+  own.load_masked(a.dw + lc.b * D, dw);
+  ownu.load_masked(a.u + lc.b * E::CDIM, u);
+  const T r = TR::kRadius ? dsqrt(Lanes<P>::sum(sumsq(x))) : T(0);
+  const Flags fl = Flags::decode(a.flag_in[lc.b]);
   const T disc = a.disc_in ? a.disc_in[lc.b] : T(1);
-  Transition<T, E, SCHEME> tr;
-  tr.run(eq, c, x, u, dw, flag, S);
-  const T cf = (T)tr.coef;
+  TR tr;
+  tr.run(eq, c, x, u, dw, fl, r);
+  const T cf = tr.coef ? T(1) : T(0);
   const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(x, u)));
+  T xn[M];
 #pragma unroll
-  for (int m = 0; m < M; ++m) a.x_out[row + m] = tr.coef ? tr.xt[m] : x[m];
+  for (int m = 0; m < M; ++m) xn[m] = tr.coef ? tr.xt[m] : x[m];
+  own.store(a.x_out + lc.b * D, xn);
   if (lc.p == 0) {
     const T yin = a.y_in ? a.y_in[lc.b] : T(0);
     if (a.y_out) a.y_out[lc.b] = yin + cost_increment(a.cost_order, w, cf, tr.dt, disc);
     if (a.disc_out) a.disc_out[lc.b] = disc * disc_factor(tr.dt, cf, c);
     if (a.dt) a.dt[lc.b] = tr.dt;
     if (a.coef) a.coef[lc.b] = cf;
-    a.flag_out[lc.b] = tr.flag_new;
+    a.flag_out[lc.b] = SCHEME == DPAC_SCHEME_ADAPTIVE ? tr.next.encode() : (tr.coef ? 1 : 0);
   }
 }
 
@@ -395,32 +485,29 @@ template <typename T, class E, int D, int SCHEME>
 __global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> c,
                                                   const StepArgs<T> a) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
-  const LaneCoord<P> lc(a.B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
-  const int64_t row = lc.b * D + lc.p * M;
-  const int64_t urow = lc.b * (MC * P) + lc.p * MC;
+  using TR = Transition<T, E, SCHEME>;
+  const LaneCoord<P> lc(a.B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+  const Own<D, P> own(lc.p);
+  const Own<E::CDIM, P> ownu(lc.p);
   T x[M], u[MC], dw[M], lam[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    x[m] = a.x[row + m];
-    dw[m] = a.dw[row + m];
-    lam[m] = a.g_x_out[row + m];
-  }
-#pragma unroll
-  for (int m = 0; m < MC; ++m) u[m] = a.u[urow + m];
-  const T S = Lanes<P>::sum(sumsq(x));
-  const int flag = a.flag_in[lc.b];
+  own.load_masked(a.x + lc.b * D, x);
+  own.load_masked(a.dw + lc.b * D, dw);
+  own.load_masked(a.g_x_out + lc.b * D, lam);
+  ownu.load_masked(a.u + lc.b * E::CDIM, u);
+  const T r = dsqrt(Lanes<P>::sum(sumsq(x)));
+  const Flags fl = Flags::decode(a.flag_in[lc.b]);
   const T disc = a.disc_in ? a.disc_in[lc.b] : T(1);
   const T gD1 = a.g_disc_out ? a.g_disc_out[lc.b] : T(0);
   const T gy1 = a.g_y_out ? a.g_y_out[lc.b] : T(0);
 
-  Transition<T, E, SCHEME> tr;
-  tr.run(eq, c, x, u, dw, flag, S);
-  const T cf = (T)tr.coef;
+  TR tr;
+  tr.run(eq, c, x, u, dw, fl, r);
+  const T cf = tr.coef ? T(1) : T(0);
   const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(x, u)));
   const T Ef = disc_factor(tr.dt, cf, c);
 
   T f[M], s[M];
-  eq.drift(x, u, S, f);
+  eq.drift(x, u, r, f);
   eq.sigma(x, u, s);
   T gx[M], gu[MC], a_f[M], a_s[M];
   T part = 0;
@@ -433,25 +520,22 @@ __global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> 
   }
 #pragma unroll
   for (int m = 0; m < MC; ++m) gu[m] = 0;
-  eq.drift_vjp(x, u, S, a_f, gx, gu);
+  eq.drift_vjp(x, u, r, a_f, gx, gu);
   eq.sigma_vjp(x, u, a_s, gx, gu);
   const T gw = gy1 * cf * tr.dt * disc;
   eq.w_vjp(x, u, gw, gx, gu);
   const T g_disc = gD1 * Ef + gy1 * cf * w * tr.dt;
   if constexpr (SCHEME == DPAC_SCHEME_ADAPTIVE) {
     const T g_dt = gD1 * disc * Ef * (c.neg_gamma * cf) + gy1 * cf * w * disc + cf * Lanes<P>::sum(part);
-    const T r = dsqrt(S);
-    const T raw = adaptive_dt_raw(flag, r, c);
-    if (flag == 1 && raw >= c.dt_min) {
+    const T raw = adaptive_dt_raw(fl.layer, r, c);
+    if (fl.layer && raw >= c.dt_min) {
       const T k = g_dt * (-(c.R - r) * c.two_inv_den) / r;
 #pragma unroll
       for (int m = 0; m < M; ++m) gx[m] += k * x[m];
     }
   }
-#pragma unroll
-  for (int m = 0; m < M; ++m) a.g_x[row + m] = gx[m];
-#pragma unroll
-  for (int m = 0; m < MC; ++m) a.g_u[urow + m] = gu[m];
+  own.store(a.g_x + lc.b * D, gx);
+  ownu.store(a.g_u + lc.b * E::CDIM, gu);
   if (a.g_disc && lc.p == 0) a.g_disc[lc.b] = g_disc;
 }
 
@@ -484,41 +568,54 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
   constexpr int P = E::kP, M = E::M, MC = E::MC, GPW = 64 / P;
   constexpr bool USE_DW = TD1 || BWD;
   constexpr bool HAS_G = TD1 && !BWD;
-  constexpr int KB = sizeof(T) == 4 ? 4 : 2;
   using F = TdFrame<T, M, MC, USE_DW && !PHILOX, HAS_G>;
+  constexpr int KB = ring_kb((int)sizeof(F), 3 * DPAC_RING_VGPRS, sizeof(T) == 4 ? 4 : 2);
   __shared__ T s_sum[kTdChunks][GPW];
   __shared__ T s_prod[kTdChunks][GPW];
 
-  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-  const LaneCoord<P> lc(a.B, lane, (int64_t)blockIdx.x * GPW);
+  // wave index is wave-uniform: say so, or the chunk loops become divergent branches
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), lane = threadIdx.x % 64;
+  const LaneCoord<P> lc(a.B, lane, xcd_block(blockIdx.x, gridDim.x) * GPW);
+  const Own<D, P> own(lc.p);
+  const Own<E::CDIM, P> ownu(lc.p);
+  const BufSlab<T, D, P> sx(own, lc.b, lc.live);         // x[t], dw[t], G[t], g_G[t] rows
+  const BufSlab<T, E::CDIM, P> su(ownu, lc.b, lc.live);  // u[t] rows
   const int g = lane / P;
-  const int64_t B = a.B;
-  const int64_t row = lc.b * D + lc.p * M;
-  const int64_t urow = lc.b * (MC * P) + lc.p * MC;
+  const int64_t B = a.B, stride = a.B * D, stride_u = a.B * E::CDIM;
+  const uint32_t slab = (uint32_t)(stride * sizeof(T)), slab_u = (uint32_t)(stride_u * sizeof(T));
   const uint64_t gtraj = (uint64_t)(a.traj_offset + lc.b);
   const int nc = (a.N + kTdChunks - 1) / kTdChunks;
   const int t_begin = min(a.N, wave * nc), t_end = min(a.N, (wave + 1) * nc);
 
+  // whole-array descriptors (host: every array < 2 GiB); the step goes in soffset
+  const uint32_t row_bytes = (uint32_t)(a.N * sizeof(T));
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(a.x, slab * (uint32_t)a.N);
+  const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(a.u, slab_u * (uint32_t)a.N);
+  const __amdgpu_buffer_rsrc_t rs_dw = make_rsrc(a.dw, (USE_DW && !PHILOX) ? slab * (uint32_t)a.N : 0u);
+  const __amdgpu_buffer_rsrc_t rs_G = make_rsrc(a.G, HAS_G ? slab * (uint32_t)a.N : 0u);
+  const __amdgpu_buffer_rsrc_t rs_gG = make_rsrc(a.g_G, BWD ? slab * (uint32_t)a.N : 0u);
+  const __amdgpu_buffer_rsrc_t rs_dt = make_rsrc(a.dt, (uint32_t)a.B * row_bytes);
+  const __amdgpu_buffer_rsrc_t rs_cf = make_rsrc(a.coef, (uint32_t)a.B * row_bytes);
+  const uint32_t off_row = (uint32_t)(lc.b * row_bytes);  // dt / coef rows are [B][N]
+  auto load_scalar = [&](__amdgpu_buffer_rsrc_t r, int t) {
+    uint32_t w[sizeof(T) / 4];
+    buf_load_dwords<sizeof(T) / 4>(r, off_row, w, (uint32_t)t * (uint32_t)sizeof(T));
+    T v;
+    __builtin_memcpy(&v, &w[0], sizeof(T));
+    return v;
+  };
   auto load = [&](int t, F& fr) {
-    const int64_t so = (int64_t)t * B;
-#pragma unroll
-    for (int m = 0; m < M; ++m) fr.x[m] = a.x[so * D + row + m];
-#pragma unroll
-    for (int m = 0; m < MC; ++m) fr.u[m] = a.u[so * (MC * P) + urow + m];
-    if constexpr (USE_DW && !PHILOX) {
-#pragma unroll
-      for (int m = 0; m < M; ++m) fr.dw[m] = a.dw[so * D + row + m];
-    }
-    if constexpr (HAS_G) {
-#pragma unroll
-      for (int m = 0; m < M; ++m) fr.G[m] = a.G[so * D + row + m];
-    }
-    fr.dt = a.dt[so + lc.b];
-    fr.coef = a.coef[so + lc.b];
+    sx.load(rs_x, fr.x, (uint32_t)t * slab);
+    su.load(rs_u, fr.u, (uint32_t)t * slab_u);
+    if constexpr (USE_DW && !PHILOX) sx.load(rs_dw, fr.dw, (uint32_t)t * slab);
+    if constexpr (HAS_G) sx.load(rs_G, fr.G, (uint32_t)t * slab);
+    fr.dt = load_scalar(rs_dt, t);
+    fr.coef = load_scalar(rs_cf, t);
   };
   auto increments = [&](int t, F& fr, T (&dwv)[M]) {
     if constexpr (PHILOX) {
       draw_owned<T, E, D>(a.seed, gtraj, t, lc.p, a.sample_type, dwv);
+      own.mask(dwv);
     } else {
 #pragma unroll
       for (int m = 0; m < M; ++m) dwv[m] = fr.dw[m];
@@ -528,16 +625,16 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
   T disc = 1;
   if constexpr (!BWD) {
     T y = 0;
-    auto body = [&](int t, F& fr) {
+    auto body = [&](int t, F& fr, auto) {
       const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(fr.x, fr.u)));
       y += cost_increment(a.cost_order, w, fr.coef, fr.dt, disc);
       if constexpr (TD1) {
         T s[M], dwv[M];
         eq.sigma(fr.x, fr.u, s);
         increments(t, fr, dwv);
-        T acc = 0;
+        T acc = (s[0] * dwv[0]) * fr.G[0];
 #pragma unroll
-        for (int m = 0; m < M; ++m) acc = fma(s[m] * dwv[m], fr.G[m], acc);
+        for (int m = 1; m < M; ++m) acc = fma(s[m] * dwv[m], fr.G[m], acc);
         const T dot = Lanes<P>::sum(acc);
         y -= (dot * disc) * (fr.coef * dsqrt(fr.dt));  // solver.py:180-184
       }
@@ -549,7 +646,7 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
       s_prod[wave][g] = disc;
     }
     __syncthreads();
-    if (wave == 0 && lc.p == 0) {
+    if (wave == 0 && lc.p == 0 && lc.live) {
       T Dw = 1, tot = 0;
 #pragma unroll
       for (int w = 0; w < kTdChunks; ++w) {
@@ -562,7 +659,7 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
   } else {
     // pass A: the chunk's discount product from (dt, coef) only
     for (int t = t_begin; t < t_end; ++t) {
-      const int64_t so = (int64_t)t * B + lc.b;
+      const int64_t so = lc.b * a.N + t;
       disc = disc * disc_factor(a.dt[so], a.coef[so], c);
     }
     if (lc.p == 0) s_prod[wave][g] = disc;
@@ -571,15 +668,15 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
     for (int w = 0; w < wave; ++w) Dw *= s_prod[w][g];
     disc = Dw;
     const T gy = a.g_y[lc.b];
-    auto body = [&](int t, F& fr) {
-      T s[M], dwv[M];
+    auto body = [&](int t, F& fr, auto) {
+      T s[M], dwv[M], out[M];
       eq.sigma(fr.x, fr.u, s);
       increments(t, fr, dwv);
       // d y / d G_j = -disc_t*coef_t*sqrt(dt_t)*diff_j
       const T k = -gy * (disc * (fr.coef * dsqrt(fr.dt)));
-      T* go = a.g_G + (int64_t)t * B * D + row;
 #pragma unroll
-      for (int m = 0; m < M; ++m) go[m] = k * (s[m] * dwv[m]);
+      for (int m = 0; m < M; ++m) out[m] = k * (s[m] * dwv[m]);
+      sx.store(rs_gG, out, (uint32_t)t * slab);
       disc = disc * disc_factor(fr.dt, fr.coef, c);
     };
     pipelined<KB, F>(t_begin, t_end, load, body);
@@ -593,41 +690,42 @@ template <typename T, class E, int D>
 __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, int64_t B,
                                               int what, const T* x, const T* u, T* out) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
-  const LaneCoord<P> lc(B, threadIdx.x, (int64_t)blockIdx.x * (64 / P));
-  const int64_t row = lc.b * D + lc.p * M;
-  const int64_t urow = lc.b * (MC * P) + lc.p * MC;
+  const LaneCoord<P> lc(B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+  const Own<D, P> own(lc.p);
+  const Own<E::CDIM, P> ownu(lc.p);
   T xv[M], uv[MC];
+  own.load_masked(x + lc.b * D, xv);
+  if (u) {
+    ownu.load_masked(u + lc.b * E::CDIM, uv);
+  } else {
 #pragma unroll
-  for (int m = 0; m < M; ++m) xv[m] = x[row + m];
-  const bool has_u = u != nullptr;
-#pragma unroll
-  for (int m = 0; m < MC; ++m) uv[m] = has_u ? u[urow + m] : T(0);
+    for (int m = 0; m < MC; ++m) uv[m] = 0;
+  }
   const T S = Lanes<P>::sum(sumsq(xv));
+  const T r = dsqrt(S);
   T v[M];
   T scalar = 0;
   bool vec = false, ctl = false;
   switch (what) {
-    case DPAC_EVAL_DRIFT: eq.drift(xv, uv, S, v); vec = true; break;
+    case DPAC_EVAL_DRIFT: eq.drift(xv, uv, r, v); vec = true; break;
     case DPAC_EVAL_SIGMA: eq.sigma(xv, uv, v); vec = true; break;
     case DPAC_EVAL_W: scalar = eq.w_finish(Lanes<P>::sum(eq.w_part(xv, uv))); break;
-    case DPAC_EVAL_Z: scalar = eq.Z(xv, S); break;
-    case DPAC_EVAL_V_TRUE: scalar = eq.V_true(xv, S); break;
+    case DPAC_EVAL_Z: scalar = eq.Z(xv, S, r); break;
+    case DPAC_EVAL_V_TRUE: scalar = eq.V_true(xv, S, r); break;
     case DPAC_EVAL_U_TRUE: {
       T uu[MC];
-      eq.u_true(xv, S, uu);
-#pragma unroll
-      for (int m = 0; m < MC; ++m) out[urow + m] = uu[m];
+      eq.u_true(xv, r, uu);
+      ownu.store(out + lc.b * E::CDIM, uu);
       ctl = true;
       break;
     }
-    case DPAC_EVAL_V_GRAD: eq.V_grad(xv, S, v); vec = true; break;
+    case DPAC_EVAL_V_GRAD: eq.V_grad(xv, S, r, v); vec = true; break;
     case DPAC_EVAL_B: scalar = S - c.R2; break;
     default: break;
   }
   if (ctl) return;
   if (vec) {
-#pragma unroll
-    for (int m = 0; m < M; ++m) out[row + m] = v[m];
+    own.store(out + lc.b * D, v);
   } else if (lc.p == 0) {
     out[lc.b] = scalar;
   }
@@ -658,17 +756,23 @@ int run_op(const OpArgs& a) {
       r.x = (T*)a.x_out; r.dt = (T*)a.dt; r.coef = (T*)a.coef; r.u = (T*)a.u_out;
       r.y = (T*)a.y; r.disc = (T*)a.disc;
       const bool philox = a.dw == nullptr, cost = a.y != nullptr;
-      constexpr int KB = sizeof(T) == 4 ? 8 : 4;
-#define DPAC_ROLL(SCH, PH, CO) \
-  hipLaunchKernelGGL((k_rollout<T, E, D, SCH, PH, CO, KB>), grid, block, 0, s, eq, c, r)
-#define DPAC_ROLL_SCH(SCH)                                                    \
-  if (philox) {                                                               \
-    if (cost) DPAC_ROLL(SCH, true, true); else DPAC_ROLL(SCH, true, false);   \
-  } else {                                                                    \
-    if (cost) DPAC_ROLL(SCH, false, true); else DPAC_ROLL(SCH, false, false); \
+      constexpr int KB_ = ring_kb((int)sizeof(DwFrame<T, E::M>), DPAC_RING_VGPRS, 8);
+      constexpr int KB = KB_ > 0 ? KB_ : 1;
+      const int out = (cost ? kOutCost : 0) | (a.u_out ? kOutU : 0);
+#define DPAC_ROLL(SCH, PH, OUT) \
+  hipLaunchKernelGGL((k_rollout<T, E, D, SCH, PH, OUT, KB>), grid, block, 0, s, eq, c, r)
+#define DPAC_ROLL_PH(SCH, PH)                              \
+  switch (out) {                                           \
+    case 0: DPAC_ROLL(SCH, PH, 0); break;                  \
+    case kOutCost: DPAC_ROLL(SCH, PH, kOutCost); break;    \
+    case kOutU: DPAC_ROLL(SCH, PH, kOutU); break;          \
+    default: DPAC_ROLL(SCH, PH, kOutCost | kOutU); break;  \
   }
+#define DPAC_ROLL_SCH(SCH) \
+  if (philox) { DPAC_ROLL_PH(SCH, true) } else { DPAC_ROLL_PH(SCH, false) }
       if (adaptive) { DPAC_ROLL_SCH(DPAC_SCHEME_ADAPTIVE) } else { DPAC_ROLL_SCH(DPAC_SCHEME_NAIVE) }
 #undef DPAC_ROLL_SCH
+#undef DPAC_ROLL_PH
 #undef DPAC_ROLL
       break;
     }

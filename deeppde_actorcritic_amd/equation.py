@@ -124,7 +124,7 @@ class Equation(object):
     # ---- rollouts ---------------------------------------------------------------
     def rollout(self, scheme: str, x0, dw, T: float, N: int, NN_control=None, cheat=False,
                 requires_grad=False):
-        """Device-native rollout: returns x [N+1,B,d], dt [N,B], coef [N,B], u [N,B,c].
+        """Device-native rollout: returns x [N+1,B,d], dt [B,N], coef [B,N], u [N,B,c].
 
         cheat=True: one fused kernel with u = u_true (equation.py:54-55/87-88).
         Otherwise u_t = NN_control(x_t) each step between dpac_step_fwd launches.
@@ -145,7 +145,7 @@ class Equation(object):
                 u = NN_control(x, False, need_grad=False)
                 x, disc, y, dt, coef, flag = ops.sde_step(eqp, sch, T, N, x, u, dw[t], flag, disc, y)
                 xs.append(x); us.append(u); dts.append(dt); coefs.append(coef)
-            return torch.stack(xs), torch.stack(dts), torch.stack(coefs), torch.stack(us)
+            return torch.stack(xs), torch.stack(dts, 1), torch.stack(coefs, 1), torch.stack(us)
         return rollout_nn_nograd(eqp, sch, x0, dw, T, N, NN_control, flag)
 
     def _propagate(self, scheme, num_sample, x0, dw_sample, NN_control, training, T, N, cheat):
@@ -154,7 +154,7 @@ class Equation(object):
         grad = (not cheat) and torch.is_grad_enabled()
         x, dt, coef, _ = self.rollout(scheme, x0, dw, T, N, NN_control, cheat, requires_grad=grad)
         # back to the reference layouts: x_smp [B,d,N+1], dt/coef [B,N]
-        return x.permute(1, 2, 0), dt.t(), coef.t()
+        return x.permute(1, 2, 0), dt, coef
 
     def propagate_naive(self, num_sample, x0, dw_sample, NN_control, training, T, N, cheat):
         """equation.py:46-71 (same signature and return layouts)."""
@@ -232,7 +232,8 @@ def rollout_nn_nograd(eqp, sch, x0, dw, T, N, NN_control, flag=None):
                       None, _lib.COST_CRITIC, ops._ptr(x[t + 1]), ops._ptr(flag2), None, None,
                       ops._ptr(dt[t]), ops._ptr(coef[t]), stream)
             flag, flag2 = flag2, flag
-    return x, dt, coef, u_all
+    # the step kernel emits per-step [B] vectors; present the [B, N] layout
+    return x, dt.t().contiguous(), coef.t().contiguous(), u_all
 
 
 class LQR(Equation):

@@ -1,7 +1,8 @@
 """Torch-facing wrappers of the libdpac C ABI (device-native layouts).
 
 Layouts (HBM, step-major): x0/x_bdry [B, d]; x [N+1, B, d]; dw, G [N, B, d];
-u [N, B, c]; dt, coef [N, B]; flags int32 [B]; y, disc [B].
+u [N, B, c]; dt, coef [B, N] (trajectory-major, the reference's own dt/coef
+layout, equation.py:70,99); flags int32 [B]; y, disc [B].
 
 Every op requires CUDA (ROCm) tensors and raises if libdpac or the GPU is
 missing: there is no CPU path in the product.
@@ -77,7 +78,7 @@ def rollout_analytic(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor | None
                      want_u: bool = False, cost_order: int | None = None, out=None):
     """Fused rollout with u = u_true (equation.py:46-106 with cheat=True).
 
-    Returns (x [N+1,B,d], dt [N,B], coef [N,B], u [N,B,c] | None, y [B] | None,
+    Returns (x [N+1,B,d], dt [B,N], coef [B,N], u [N,B,c] | None, y [B] | None,
     disc [B] | None).  dw=None draws increments in-kernel from the Philox stream.
     """
     _require_gpu(x0, dw)
@@ -89,8 +90,8 @@ def rollout_analytic(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor | None
     kw = dict(dtype=x0.dtype, device=x0.device)
     if out is None:
         x = torch.empty(N + 1, B, d, **kw)
-        dt = torch.empty(N, B, **kw)
-        coef = torch.empty(N, B, **kw)
+        dt = torch.empty(B, N, **kw)
+        coef = torch.empty(B, N, **kw)
     else:
         x, dt, coef = out
     u = torch.empty(N, B, eqp.control_dim, **kw) if want_u else None
@@ -171,7 +172,7 @@ class _TdAssemble(torch.autograd.Function):
     @staticmethod
     def forward(ctx, G, x, u, dw, dt, coef, eqp, td_type, cost_order, seed, traj_offset,
                 sample_type):
-        N, B = dt.shape
+        B, N = dt.shape
         y = torch.empty(B, dtype=x.dtype, device=x.device)
         disc = torch.empty_like(y)
         call("dpac_td_assemble_fwd", ctypes.byref(eqp), td_type, cost_order, _dtype_id(x), B, N,
@@ -188,7 +189,7 @@ class _TdAssemble(torch.autograd.Function):
         eqp, td_type, seed, traj_offset, sample_type, has_g = ctx.cfg
         gG = None
         if has_g and td_type == _lib.TD1 and g_y is not None and ctx.needs_input_grad[0]:
-            N, B = dt.shape
+            B, N = dt.shape
             gG = torch.empty(N, B, eqp.dim, dtype=x.dtype, device=x.device)
             call("dpac_td_assemble_bwd", ctypes.byref(eqp), _dtype_id(x), B, N, _ptr(x),
                  _ptr(u), _ptr(dw), seed & 0xFFFFFFFFFFFFFFFF, traj_offset, sample_type,
@@ -214,7 +215,7 @@ def td_assemble(eqp, td_type: int, x, u, dw, dt, coef, G=None, *,
 def actor_cost(eqp, x, u, dt, coef):
     """Σ_t coef·w·dt·disc and disc_N over a finished trajectory (solver.py:213-219)."""
     _require_gpu(x, u, dt, coef)
-    N, B = dt.shape
+    B, N = dt.shape
     y = torch.empty(B, dtype=x.dtype, device=x.device)
     disc = torch.empty_like(y)
     call("dpac_actor_cost_fwd", ctypes.byref(eqp), _dtype_id(x), B, N, _ptr(x.contiguous()),

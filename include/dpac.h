@@ -24,13 +24,21 @@
  *    an unsupported (equation, dim) combination, otherwise the hipError_t of the
  *    failed launch.  dpac_last_error() returns a thread-local message.
  *
- * HBM layouts (step-major, one trajectory row per step; B = num_sample,
- * d = dim, c = control_dim, N = num_steps):
+ * HBM layouts (B = num_sample, d = dim, c = control_dim, N = num_steps).  State,
+ * noise and control are step-major (one [B][d] slab per step, read/written as a
+ * unit by every step of the time loop); the per-step scalars dt and coef are
+ * trajectory-major, exactly the reference's dt[B,N] / coef[B,N]
+ * (equation.py:70,99):
  *    x0, x_bdry  [B][d]            x     [N+1][B][d]      dw  [N][B][d]
- *    u           [N][B][c]         dt    [N][B]           coef [N][B]
+ *    u           [N][B][c]         dt    [B][N]           coef [B][N]
  *    G           [N][B][d]         flag  [B] (int32)      y, disc [B]
- * The reference keeps x_smp as [B][d][N+1], dw as [B][d][N] (equation.py:19,50,68);
- * the Python shims transpose only at the parity boundary.
+ * The single-step entry points (dpac_step_fwd/bwd) take and return one step's
+ * [B] vectors.  The reference keeps x_smp as [B][d][N+1] and dw as [B][d][N]
+ * (equation.py:19,50,68); the Python shims transpose only at the parity boundary.
+ * Limit: B·(N+1)·max(d,c)·sizeof(T) must stay below 2 GiB (each array is
+ * addressed through one 32-bit buffer descriptor); else DPAC_EINVAL.  Larger
+ * batches are split over launches; traj_offset keeps the in-kernel noise of
+ * every trajectory the same under any split.
  */
 #ifndef DPAC_H_
 #define DPAC_H_

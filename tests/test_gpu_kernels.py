@@ -48,9 +48,9 @@ def test_rollout_matches_golden_fp64(path):
     N, T = int(g["N"]), float(g["T"])
     for order, key in ((_lib.COST_CRITIC, "y_critic"), (_lib.COST_ACTOR, "y_actor")):
         x, dt, coef, u, y, disc = ops.rollout_analytic(eqp, sch, x0, dw, T, N, want_u=True, cost_order=order)
-        np.testing.assert_array_equal(coef.t().cpu().numpy(), g["coef"])
+        np.testing.assert_array_equal(coef.cpu().numpy(), g["coef"])
         assert rel_close(x.permute(1, 2, 0).cpu(), g["x"], 1e-12)
-        assert rel_close(dt.t().cpu(), g["dt"], 1e-12)
+        assert rel_close(dt.cpu(), g["dt"], 1e-12)
         assert rel_close(y.cpu(), g[key], 1e-12)
         assert rel_close(disc.cpu(), g["disc"], 1e-12)
 
@@ -68,9 +68,9 @@ def test_rollout_vs_oracle_fp64(name, d, scheme, sample):
     xr, dtr, cr = prop(B, x0, dw, None, False, T, N, True)
     x, dt, coef, u, y, disc = ops.rollout_analytic(ep.params(), SCHEMES[scheme], dev(x0), native_dw(dw), T, N,
                                                    want_u=True, cost_order=_lib.COST_CRITIC)
-    np.testing.assert_array_equal(coef.t().cpu().numpy(), cr.numpy())
+    np.testing.assert_array_equal(coef.cpu().numpy(), cr.numpy())
     assert rel_close(x.permute(1, 2, 0).cpu(), xr, 1e-12)
-    assert rel_close(dt.t().cpu(), dtr, 1e-12)
+    assert rel_close(dt.cpu(), dtr, 1e-12)
     ur = torch.stack([eo.u_true(xr[:, :, t]) for t in range(N)])
     assert rel_close(u.cpu(), ur, 1e-12)
 
@@ -88,12 +88,12 @@ def test_rollout_fp32_within_tolerance(name, d, scheme):
     x, dt, coef, _, y, disc = ops.rollout_analytic(ep.params(), SCHEMES[scheme], dev(x0, torch.float32),
                                                    native_dw(dw, torch.float32), T, N,
                                                    cost_order=_lib.COST_ACTOR)
-    c = coef.t().cpu().numpy()
+    c = coef.cpu().numpy()
     same = np.all(c == cr.numpy(), axis=1)
     assert np.mean(~same) <= 1e-3, f"{np.mean(~same):.2e} of trajectories flipped an exit decision"
     xm = x.permute(1, 2, 0).cpu().double().numpy()[same]
     assert rel_close(xm, xr.numpy()[same], 2e-5)
-    assert rel_close(dt.t().cpu().double().numpy()[same], dtr.numpy()[same], 2e-5)
+    assert rel_close(dt.cpu().double().numpy()[same], dtr.numpy()[same], 2e-5)
 
 
 @pytest.mark.parametrize("name,d", CASES)
@@ -153,7 +153,7 @@ def test_td_assemble_fwd_bwd_vs_oracle(name, d, td, scheme):
     Gd = G.detach().to(DEV).requires_grad_(True)
     tdt = _lib.TD1 if td == "TD1" else _lib.TD2
     yp, discp = ops.td_assemble(ep.params(), tdt, xr.permute(2, 0, 1).contiguous().to(DEV), U.to(DEV),
-                                native_dw(dw), dtr.t().contiguous().to(DEV), cr.t().contiguous().to(DEV),
+                                native_dw(dw), dtr.contiguous().to(DEV), cr.contiguous().to(DEV),
                                 Gd if td == "TD1" else None)
     assert rel_close(yp.detach().cpu(), y.detach()[:, 0], 1e-12)
     assert rel_close(discp.cpu(), disc[:, 0], 1e-12)
@@ -240,9 +240,9 @@ def test_full_size_invariants_and_sharding(scheme):
     # every recorded state strictly inside the ball; coef in {0,1}, non-increasing in t
     assert float(torch.linalg.norm(x, dim=2).max()) < 1.0
     assert set(torch.unique(coef).tolist()).issubset({0.0, 1.0})
-    assert bool(torch.all(coef[1:] <= coef[:-1]))
+    assert bool(torch.all(coef[:, 1:] <= coef[:, :-1]))
     # frozen after exit: x_{t+1} == x_t wherever coef_t == 0
-    frozen = coef == 0
+    frozen = (coef == 0).t()  # [N, B] like x[1:]
     assert torch.equal(x[1:][frozen], x[:-1][frozen])
     dt0 = 0.2 / N
     if scheme == "naive":
@@ -250,13 +250,13 @@ def test_full_size_invariants_and_sharding(scheme):
     else:
         assert float(dt.min()) >= dt0 * 1e-4 * (1 - 1e-6) and float(dt.max()) <= dt0 * (1 + 1e-6)
     # discount consistent with sum of coef*dt: disc = prod exp(-g dt coef)
-    ref = torch.exp(-(dt.double() * coef.double()).sum(0))
+    ref = torch.exp(-(dt.double() * coef.double()).sum(1))
     assert torch.allclose(disc.double(), ref, rtol=1e-5)
     # sharding: rows of a half batch rolled out alone are bit-identical
     h = B // 2
     xs, dts, cs, _, ys, ds = ops.rollout_analytic(eqp, SCHEMES[scheme], x0[h:].contiguous(), dw[:, h:].contiguous(),
                                                   0.2, N, cost_order=_lib.COST_ACTOR)
-    assert torch.equal(xs, x[:, h:]) and torch.equal(cs, coef[:, h:]) and torch.equal(ys, y[h:])
+    assert torch.equal(xs, x[:, h:]) and torch.equal(cs, coef[h:]) and torch.equal(ys, y[h:])
 
 
 def test_odd_batch_sizes():
@@ -272,5 +272,5 @@ def test_odd_batch_sizes():
             x0, dw, _ = eo.sample_normal(B, 12)
         xr, dtr, cr = eo.propagate_adaptive(B, x0, dw, None, False, 0.2, 12, True)
         x, dt, coef, *_ = ops.rollout_analytic(ep.params(), 1, dev(x0), native_dw(dw), 0.2, 12)
-        np.testing.assert_array_equal(coef.t().cpu().numpy(), cr.numpy())
+        np.testing.assert_array_equal(coef.cpu().numpy(), cr.numpy())
         assert rel_close(x.permute(1, 2, 0).cpu(), xr, 1e-12)

@@ -1,0 +1,4 @@
+source tools/gpu_steps.sh
+for v in kb4 kb8 kb12 kb16 nostore noload; do
+  DPAC_LIB=$PWD/tools/variants/libdpac_$v.so run 200 var_$v python tools/probe_rollout.py --B 4096,16384 --N 200 --reps 100
+done
