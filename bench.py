@@ -47,23 +47,26 @@ def barrier(world):
 
 
 def time_launches(launch, steps, warmup, world):
-    """Warm up, then time exactly `steps` launches between barrier+synchronize pairs.
-    Also brackets every launch with HIP events on the launch stream."""
+    """Warm up, then time exactly `steps` back-to-back launches between
+    barrier+synchronize pairs.  A HIP event pair on the launch stream (torch's
+    current stream, which every launch here uses) brackets the same launches:
+    per-launch time = event span / steps, i.e. kernel time plus the dispatch gap
+    between consecutive launches (rocprofv3's per-kernel average excludes it)."""
     for _ in range(warmup):
         launch()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record()
+    start.record()
+    for _ in range(steps):
         launch()
-        e.record()
+    end.record()
     torch.cuda.synchronize()
     barrier(world)
     wall = time.perf_counter() - t0
-    per_launch_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    per_launch_ms = start.elapsed_time(end) / steps
     return wall, per_launch_ms
 
 

@@ -33,12 +33,19 @@ def main(tag):
     ks = os.path.join(OUT, "prof_kt", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    bl = os.path.join(OUT, "bench.log")
+    if os.path.exists(bl):
+        lines = [l for l in open(bl) if l.startswith("{")]
+        if lines:
+            with open(os.path.join(PROF, f"{tag}_bench.jsonl"), "a") as f:
+                f.write(lines[-1])
     f = os.path.join(OUT, "pmc_fetch", "run_counter_collection.csv")
     w = os.path.join(OUT, "pmc_write", "run_counter_collection.csv")
     if not (os.path.exists(f) and os.path.exists(w)):
         print("no PMC passes found")
         return
-    key_kernel = "k_rollout<float, dpac::EqLQR<float, 20, 4>, 20, 1, false, false"
+    # canonical rollout: f32, LQR d=20 (16 lanes/trajectory), adaptive, dw from HBM, no cost/u outputs
+    key_kernel = "k_rollout<float, dpac::EqLQR<float, 20, 16>, 20, 1, false, 0,"
     fetch_kib, nf, row = counter_mean(f, key_kernel, "FETCH_SIZE")
     write_kib, nw, _ = counter_mean(w, key_kernel, "WRITE_SIZE")
     fetch_b = fetch_kib * 1024 * 2  # gfx950: FETCH_SIZE counts 64 B per 128-B request

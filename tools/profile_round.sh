@@ -1,7 +1,14 @@
+#!/usr/bin/env bash
+# One round's GPU evidence: GPU tests, bench line, rocprofv3 kernel trace and the
+# two HBM counter passes (FETCH_SIZE, WRITE_SIZE in separate runs, as
+# MI355X_MICROARCH.md §HBM prescribes).  Run on the GPU box:
+#   gpurun -- 'bash tools/profile_round.sh'   then   python tools/collect_profiles.py rNN
 source tools/gpu_steps.sh
 export TMPDIR=/tmp
 R=$PWD
-run 900 pytest_gpu python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider
+rm -f gpurun_out/steps.log
+rm -rf gpurun_out/prof_kt gpurun_out/pmc_fetch gpurun_out/pmc_write
+run 900 pytest_gpu python -m pytest tests -m gpu -q -p no:cacheprovider
 run 300 bench python bench.py --steps 200 --warmup 20
 run 300 prof_kt rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline
 run 300 pmc_fetch rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
