@@ -1,0 +1,132 @@
+#!/usr/bin/env python3
+"""Training-level parity on lqr_d20: err_value (solver.py:109-113) of the product
+(GPU, fp32 and fp64) against the float64 CPU oracle, same initial weights and the
+same host-sampled numpy stream (solver.py:36-71 run verbatim).
+
+    python tools/train_check.py --iters 200 --log-freq 50 --runs gpu32,gpu64,oracle \
+        --out gpurun_out/train_check.json
+
+lqr_d20 is the reference's configs/lqr_d20.json (values restated below): d = c = 20,
+N = 100, T = 0.2, 3x200 MLPs, batch = valid = 2048, adaptive scheme, TD1, normal
+sampling, actor-critic.  --iters / --log-freq shorten the 50 000-iteration run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from deeppde_actorcritic_amd import equation as peq  # noqa: E402
+from deeppde_actorcritic_amd import solver as psol  # noqa: E402
+from deeppde_actorcritic_amd.config import munchify  # noqa: E402
+
+
+def lqr_d20(iters, log_freq, dtype, batch, valid):
+    return munchify({
+        "eqn_config": {"_comment": "linear quadratic regulator", "eqn_name": "LQR",
+                       "total_time_critic": 0.2, "total_time_actor": 0.2, "dim": 20, "control_dim": 20,
+                       "num_time_interval_critic": 100, "num_time_interval_actor": 100,
+                       "discount": 1.0, "p": 1.0, "q": 1.0, "beta": 1.0, "R": 1.0},
+        "net_config": {"num_hiddens_critic": [200, 200, 200], "num_hiddens_actor": [200, 200, 200],
+                       "lr_values_critic": [1e-3, 1e-4, 1e-5], "lr_boundaries_critic": [30000, 40000],
+                       "lr_values_actor": [1e-3, 1e-4, 1e-5], "lr_boundaries_actor": [30000, 40000],
+                       "num_iterations": iters, "batch_size": batch, "valid_size": valid,
+                       "logging_frequency": log_freq, "dtype": dtype, "verbose": False},
+        "train_config": {"sample_type": "normal", "scheme": "adaptive", "TD_type": "TD1",
+                         "train": "actor-critic"},
+    })
+
+
+COLS = ["step", "loss_critic", "loss_actor", "err_value", "err_value_infty", "err_control",
+        "err_value_grad", "err_cost", "elapsed"]
+
+
+def history_dict(h):
+    h = np.asarray(h)[:-1]  # last row is the true-loss-actor record (solver.py:62)
+    return {c: h[:, i].tolist() for i, c in enumerate(COLS)}
+
+
+def heartbeat(period=60.0):
+    """Print a line every `period` s so a long CPU-oracle run never looks hung."""
+    import threading
+    t0 = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"... {time.perf_counter() - t0:.0f} s", flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
+def main():
+    heartbeat()
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--log-freq", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--valid", type=int, default=2048)
+    ap.add_argument("--runs", default="gpu32,gpu64,oracle")
+    ap.add_argument("--seed", type=int, default=11, help="weight-initialisation seed")
+    ap.add_argument("--data-seed", type=int, default=123, help="np.random.seed before train()")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "train_check.json"))
+    a = ap.parse_args()
+    runs = a.runs.split(",")
+    res = {"config": "lqr_d20 (configs/lqr_d20.json values)", "iters": a.iters, "log_freq": a.log_freq,
+           "batch": a.batch, "valid": a.valid, "runs": {}}
+    init = None
+    for run in runs:
+        if run == "oracle":
+            continue
+        dtype = "float32" if run == "gpu32" else "float64"
+        cfg = lqr_d20(a.iters, a.log_freq, dtype, a.batch, a.valid)
+        bsde = peq.LQR(cfg.eqn_config)
+        sp = psol.ActorCriticSolver(cfg, bsde, seed=a.seed, sampler="host")
+        if init is None:  # every run starts from the first run's weights, in float64
+            init = {"critic": sp.model_critic.NN_value.export_params(),
+                    "critic_grad": sp.model_critic.NN_value_grad.export_params(),
+                    "actor": sp.model_actor.NN_control.export_params()}
+        else:
+            sp.model_critic.NN_value.load_params(init["critic"])
+            sp.model_critic.NN_value_grad.load_params(init["critic_grad"])
+            sp.model_actor.NN_control.load_params(init["actor"])
+        np.random.seed(a.data_seed)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h = sp.train()[0]
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        res["runs"][run] = {"history": history_dict(h), "wall_s": wall, "dtype": dtype}
+        print(json.dumps({"run": run, "wall_s": wall, "err_value": res["runs"][run]["history"]["err_value"]}),
+              flush=True)
+    if "oracle" in runs:
+        from oracle import equations as oeq
+        from oracle import solver as osol
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        cfg = lqr_d20(a.iters, a.log_freq, "float64", a.batch, a.valid)
+        so = osol.ActorCriticSolver(cfg, oeq.make(cfg.eqn_config), params=init)
+        np.random.seed(a.data_seed)
+        t0 = time.perf_counter()
+        h = so.train()
+        wall = time.perf_counter() - t0
+        res["runs"]["oracle"] = {"history": history_dict(h), "wall_s": wall, "dtype": "float64",
+                                 "threads": torch.get_num_threads()}
+        print(json.dumps({"run": "oracle", "wall_s": wall, "err_value": res["runs"]["oracle"]["history"]["err_value"]}),
+              flush=True)
+    if "oracle" in res["runs"]:
+        ref = np.array(res["runs"]["oracle"]["history"]["err_value"])
+        res["max_abs_err_value_diff_vs_oracle"] = {
+            r: float(np.max(np.abs(np.array(v["history"]["err_value"]) - ref)))
+            for r, v in res["runs"].items() if r != "oracle"}
+        print(json.dumps(res["max_abs_err_value_diff_vs_oracle"]), flush=True)
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    json.dump(res, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
