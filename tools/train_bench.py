@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""End-to-end training throughput on lqr_d20 (GPU only): wall time per
+iteration = one critic step + one actor step (solver.py:67-70) on fresh
+on-device samples, validation excluded.
+
+    python tools/train_bench.py [--iters 20] [--warmup 3] [--dtype float32] [--batch 2048]
+
+Prints one JSON line: ms per iteration (critic / actor split) and the rollout
+trajectory-steps per second it implies (2 rollouts of B x N per iteration).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from deeppde_actorcritic_amd import equation as peq  # noqa: E402
+from deeppde_actorcritic_amd import solver as psol  # noqa: E402
+from tools.train_check import lqr_d20  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--batch", type=int, default=2048)
+    a = ap.parse_args()
+    cfg = lqr_d20(a.iters, 10 ** 9, a.dtype, a.batch, a.batch)
+    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=1, sampler="device")
+    B, N = a.batch, cfg.eqn_config.num_time_interval_critic
+
+    def critic():
+        sp.train_step_critic(sp.sample(B, N))
+
+    def actor():
+        sp.train_step_actor(sp.sample(B, N))
+
+    for _ in range(a.warmup):
+        critic()
+        actor()
+    torch.cuda.synchronize()
+    tc = ta = 0.0
+    for _ in range(a.iters):
+        t0 = time.perf_counter()
+        critic()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        actor()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        tc += t1 - t0
+        ta += t2 - t1
+    ms = (tc + ta) / a.iters * 1e3
+    print(json.dumps({"config": "lqr_d20", "dtype": a.dtype, "batch": B, "N": N, "iters": a.iters,
+                      "ms_per_iter": ms, "critic_ms": tc / a.iters * 1e3, "actor_ms": ta / a.iters * 1e3,
+                      "traj_steps_per_s": 2 * B * N / (ms * 1e-3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
