@@ -48,6 +48,22 @@ class EqnParams(ctypes.Structure):
     ]
 
 
+MLP_MAX_HIDDEN, MLP_MAX_WIDTH = 4, 256
+
+
+class Mlp(ctypes.Structure):
+    """dpac_mlp (include/dpac.h): the actor MLP of dpac_rollout_nn_fwd."""
+
+    _fields_ = [
+        ("n_hidden", ctypes.c_int32), ("ekn_head", ctypes.c_int32),
+        ("width", ctypes.c_int32 * (MLP_MAX_HIDDEN + 2)),
+        ("bn_scale", ctypes.c_void_p * (MLP_MAX_HIDDEN + 2)),
+        ("bn_shift", ctypes.c_void_p * (MLP_MAX_HIDDEN + 2)),
+        ("weight", ctypes.c_void_p * (MLP_MAX_HIDDEN + 1)),
+        ("bias", ctypes.c_void_p),
+    ]
+
+
 _P = ctypes.c_void_p
 _I32, _I64, _U64, _D = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 _EQ = ctypes.POINTER(EqnParams)
@@ -71,6 +87,8 @@ SIGNATURES = {
                              _P],
     "dpac_actor_cost_fwd": [_EQ, _I32, _I64, _I32, _P, _P, _P, _P, _P, _P, _P],
     "dpac_equation_eval": [_EQ, _I32, _I32, _I64, _P, _P, _P, _P],
+    "dpac_rollout_nn_fwd": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp), _P, _P, _P, _P,
+                            _P, _P, _I32, _P, _P, _P, _P, _P, _P],
 }
 _RESTYPES = {"dpac_abi_version": ctypes.c_int32, "dpac_last_error": ctypes.c_char_p,
              "dpac_supported": ctypes.c_int32}

@@ -30,6 +30,7 @@ enum Op : int {
   OP_TD_FWD,
   OP_TD_BWD,
   OP_EVAL,
+  OP_ROLLOUT_NN,
 };
 
 // Everything any op may need; unused fields are ignored.
@@ -47,6 +48,9 @@ struct OpArgs {
   void *x_out, *dt, *coef, *u_out, *y, *disc, *disc_out, *y_out;
   int32_t* flag_out;
   void *g_x, *g_u, *g_disc, *g_G, *out;
+  dpac_mlp mlp;                  // OP_ROLLOUT_NN: the actor MLP
+  void *save_z, *save_disc;      // OP_ROLLOUT_NN: optional backward saves
+  int32_t* save_flag;
   hipStream_t stream;
 };
 
@@ -731,6 +735,8 @@ __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, i
   }
 }
 
+#include "dpac_rollout_nn.h"
+
 // ---------------------------------------------------------------------------
 // Launcher for one (T, equation functor, D).
 // ---------------------------------------------------------------------------
@@ -830,6 +836,39 @@ int run_op(const OpArgs& a) {
       hipLaunchKernelGGL((k_eval<T, E, D>), grid, block, 0, s, eq, c, a.B, a.what,
                          (const T*)a.x, (const T*)a.u, (T*)a.out);
       break;
+    case OP_ROLLOUT_NN: {
+      NnMlp<T> m{};
+      m.L = a.mlp.n_hidden;
+      m.ekn = a.mlp.ekn_head;
+      int z = 0;
+      for (int i = 0; i <= m.L + 1; ++i) {
+        m.width[i] = a.mlp.width[i];
+        m.scale[i] = (const T*)a.mlp.bn_scale[i];
+        m.shift[i] = (const T*)a.mlp.bn_shift[i];
+        m.zoff[i] = i == 0 ? 0 : z;
+        if (i > 0) z += m.width[i];
+      }
+      m.ztot = z;
+      for (int i = 0; i <= m.L; ++i) m.weight[i] = (const T*)a.mlp.weight[i];
+      m.bias = (const T*)a.mlp.bias;
+      NnRolloutArgs<T> r{};
+      r.B = a.B; r.N = a.N; r.cost_order = a.cost_order;
+      r.x0 = (const T*)a.x0; r.dw = (const T*)a.dw;
+      r.x = (T*)a.x_out; r.dt = (T*)a.dt; r.coef = (T*)a.coef; r.u = (T*)a.u_out;
+      r.y = (T*)a.y; r.disc = (T*)a.disc;
+      r.save_z = (T*)a.save_z; r.save_disc = (T*)a.save_disc; r.save_flag = a.save_flag;
+      const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
+      const bool cost = a.y != nullptr;
+#define DPAC_ROLL_NN(SCH, CO) \
+  hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1>), ngrid, nblock, 0, s, eq, c, m, r)
+      if (adaptive) {
+        if (cost) DPAC_ROLL_NN(DPAC_SCHEME_ADAPTIVE, true); else DPAC_ROLL_NN(DPAC_SCHEME_ADAPTIVE, false);
+      } else {
+        if (cost) DPAC_ROLL_NN(DPAC_SCHEME_NAIVE, true); else DPAC_ROLL_NN(DPAC_SCHEME_NAIVE, false);
+      }
+#undef DPAC_ROLL_NN
+      break;
+    }
     default:
       return DPAC_EINVAL;
   }

@@ -127,7 +127,9 @@ class Equation(object):
         """Device-native rollout: returns x [N+1,B,d], dt [B,N], coef [B,N], u [N,B,c].
 
         cheat=True: one fused kernel with u = u_true (equation.py:54-55/87-88).
-        Otherwise u_t = NN_control(x_t) each step between dpac_step_fwd launches.
+        NN control without gradients: one fused kernel evaluating the actor MLP on
+        MFMA tiles inside the time loop (dpac_rollout_nn_fwd).  With gradients
+        (the actor's BPTT): u_t = NN_control(x_t) between dpac_step_fwd launches.
         """
         sch = SCHEMES[scheme]
         eqp = self.params()
@@ -135,8 +137,8 @@ class Equation(object):
             x, dt, coef, u, _, _ = ops.rollout_analytic(eqp, sch, x0, dw, T, N, want_u=True)
             return x, dt, coef, u
         B = x0.shape[0]
-        flag = ops.flag_init(eqp, sch, x0, T, N)
         if requires_grad:
+            flag = ops.flag_init(eqp, sch, x0, T, N)
             xs, us, dts, coefs = [x0], [], [], []
             disc = torch.ones(B, dtype=x0.dtype, device=x0.device)
             y = torch.zeros_like(disc)
@@ -146,7 +148,11 @@ class Equation(object):
                 x, disc, y, dt, coef, flag = ops.sde_step(eqp, sch, T, N, x, u, dw[t], flag, disc, y)
                 xs.append(x); us.append(u); dts.append(dt); coefs.append(coef)
             return torch.stack(xs), torch.stack(dts, 1), torch.stack(coefs, 1), torch.stack(us)
-        return rollout_nn_nograd(eqp, sch, x0, dw, T, N, NN_control, flag)
+        view = NN_control.mlp_view() if hasattr(NN_control, "mlp_view") else None
+        if view is not None and view.supported():  # one fused launch, MLP on MFMA
+            x, dt, coef, u, _, _, _ = ops.rollout_nn(eqp, sch, x0, dw, T, N, view)
+            return x, dt, coef, u
+        return rollout_nn_nograd(eqp, sch, x0, dw, T, N, NN_control)
 
     def _propagate(self, scheme, num_sample, x0, dw_sample, NN_control, training, T, N, cheat):
         x0 = _as_dev(x0).contiguous()

@@ -106,6 +106,70 @@ def rollout_analytic(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor | None
     return x, dt, coef, u, y, disc
 
 
+class MlpView:
+    """The actor MLP as dpac_rollout_nn_fwd reads it (include/dpac.h dpac_mlp).
+
+    `tensors` keeps every device buffer the struct points to alive; all must be
+    contiguous, on the GPU, in the rollout's dtype."""
+
+    def __init__(self, scales, shifts, weights, bias, ekn_head: bool):
+        L = len(weights) - 1
+        if not 1 <= L <= _lib.MLP_MAX_HIDDEN:
+            raise ValueError(f"the fused rollout supports 1..{_lib.MLP_MAX_HIDDEN} hidden layers, got {L}")
+        self.tensors = [t.contiguous() for t in list(scales) + list(shifts) + list(weights) + [bias]]
+        sc, sh = self.tensors[:L + 2], self.tensors[L + 2:2 * L + 4]
+        ws, b = self.tensors[2 * L + 4:3 * L + 5], self.tensors[-1]
+        m = _lib.Mlp()
+        m.n_hidden, m.ekn_head = L, int(bool(ekn_head))
+        m.width[0] = ws[0].shape[0]
+        for i, w in enumerate(ws):
+            m.width[i + 1] = w.shape[1]
+            m.weight[i] = w.data_ptr()
+        for i in range(L + 2):
+            m.bn_scale[i], m.bn_shift[i] = sc[i].data_ptr(), sh[i].data_ptr()
+        m.bias = b.data_ptr()
+        self.struct = m
+        self.widths = [m.width[i] for i in range(L + 2)]
+
+    def supported(self) -> bool:
+        return max(self.widths) <= _lib.MLP_MAX_WIDTH
+
+
+def rollout_nn(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor, total_time: float,
+               num_steps: int, mlp: MlpView, *, want_u: bool = True, cost_order: int | None = None,
+               save: bool = False):
+    """Fused rollout with u_t = actor MLP(x_t) (equation.py:46-106 with NN_control,
+    solver.py:260-278), one launch of dpac_rollout_nn_fwd.
+
+    Returns (x [N+1,B,d], dt [B,N], coef [B,N], u [N,B,c] | None, y | None, disc | None,
+    saves | None) with saves = (z [N,B,Σ widths[1:]], flag [N,B] int32, disc_t [N,B])."""
+    _require_gpu(x0, dw, *mlp.tensors)
+    _check_same(x0, dw, *mlp.tensors)
+    B, d = x0.shape
+    N = num_steps
+    if tuple(dw.shape) != (N, B, d):
+        raise ValueError(f"dw must be [N, B, d] = {(N, B, d)}, got {tuple(dw.shape)}")
+    kw = dict(dtype=x0.dtype, device=x0.device)
+    x = torch.empty(N + 1, B, d, **kw)
+    dt = torch.empty(B, N, **kw)
+    coef = torch.empty(B, N, **kw)
+    u = torch.empty(N, B, eqp.control_dim, **kw) if want_u else None
+    y = disc = None
+    if cost_order is not None:
+        y = torch.empty(B, **kw)
+        disc = torch.empty(B, **kw)
+    saves = None
+    if save:
+        saves = (torch.empty(N, B, sum(mlp.widths[1:]), **kw),
+                 torch.empty(N, B, dtype=torch.int32, device=x0.device), torch.empty(N, B, **kw))
+    call("dpac_rollout_nn_fwd", ctypes.byref(eqp), scheme, _dtype_id(x0), B, N, float(total_time),
+         ctypes.byref(mlp.struct), _ptr(x0.contiguous()), _ptr(dw.contiguous()), _ptr(x), _ptr(dt),
+         _ptr(coef), _ptr(u), _lib.COST_CRITIC if cost_order is None else cost_order, _ptr(y),
+         _ptr(disc), _ptr(saves[0] if saves else None), _ptr(saves[1] if saves else None),
+         _ptr(saves[2] if saves else None), _stream(x0))
+    return x, dt, coef, u, y, disc, saves
+
+
 def flag_init(eqp, scheme: int, x0: torch.Tensor, total_time: float, num_steps: int):
     _require_gpu(x0)
     flag = torch.empty(x0.shape[0], dtype=torch.int32, device=x0.device)

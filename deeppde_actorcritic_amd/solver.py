@@ -94,6 +94,14 @@ class DeepNN(nn.Module):
             y = y[:, 0:d] / (1e-15 + torch.relu(y[:, d:d + 1]) + norm_y)
         return y
 
+    @torch.no_grad()
+    def mlp_view(self):
+        """This network as dpac_rollout_nn_fwd reads it (BN scale = rs * gamma, the same
+        product forward() forms)."""
+        rs = self.bn_rs
+        return ops.MlpView([rs * g for g in self.bn_gamma], [bt.detach() for bt in self.bn_beta],
+                           [w.detach() for w in self.W], self.b.detach(), self.ekn_head)
+
     def trainable_variables(self):
         return list(self.bn_gamma) + list(self.bn_beta) + list(self.W) + [self.b]
 

@@ -217,6 +217,43 @@ int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
                         const void* u, const void* dt, const void* coef,
                         void* y, void* disc, void* stream);
 
+/* ---- rollout with the actor MLP as control, fused (one launch) ----------
+ * equation.py:46-106 with u_t = NN_control(x_t) (solver.py:260-278) evaluated
+ * inside the time loop on MFMA tiles.  The MLP is bn_0 -> (dense -> bn -> y+relu(y))
+ * x n_hidden -> dense(+bias) -> bn_last [-> Eikonal head], with the weights of
+ * `dpac_mlp` in the call's dtype:
+ *   width[0] = dim, width[1..n_hidden] = hidden widths, width[n_hidden+1] = out
+ *     (control_dim, or control_dim + 1 with ekn_head, solver.py:255-274);
+ *   bn_scale[i] = gamma_i / sqrt(1 + 1e-6), bn_shift[i] = beta_i, [width[i]],
+ *     i = 0..n_hidden+1 (BatchNormalization in inference form, solver.py:239-245);
+ *   weight[i] = [width[i]][width[i+1]] row-major (x @ W), i = 0..n_hidden;
+ *   bias = [out].
+ * 1 <= n_hidden <= DPAC_MLP_MAX_HIDDEN, every width <= DPAC_MLP_MAX_WIDTH.
+ * Outputs as dpac_rollout_fwd, with u [N][B][c] the control actually applied.
+ * y/disc (optional, both or neither): the pathwise cost in `cost_order`.
+ * Backward saves (optional, all or none): save_z [N][B][Σ_{i>=1} width[i]] the
+ * pre-BN output of every dense layer (layer i at column offset
+ * Σ_{1<=k<i} width[k]), save_flag [N][B] and save_disc [N][B] the flag and the
+ * discount entering step t. */
+#define DPAC_MLP_MAX_HIDDEN 4
+#define DPAC_MLP_MAX_WIDTH 256
+typedef struct dpac_mlp {
+  int32_t n_hidden;
+  int32_t ekn_head;
+  int32_t width[DPAC_MLP_MAX_HIDDEN + 2];
+  const void* bn_scale[DPAC_MLP_MAX_HIDDEN + 2];
+  const void* bn_shift[DPAC_MLP_MAX_HIDDEN + 2];
+  const void* weight[DPAC_MLP_MAX_HIDDEN + 1];
+  const void* bias;
+} dpac_mlp;
+
+int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                        int64_t num_sample, int32_t num_steps, double total_time,
+                        const dpac_mlp* actor, const void* x0, const void* dw, void* x,
+                        void* dt, void* coef, void* u, int32_t cost_order, void* y,
+                        void* disc, void* save_z, int32_t* save_flag, void* save_disc,
+                        void* stream);
+
 /* ---- device equation coefficients (for parity tests and metrics) -------
  * Evaluates one Equation method row-wise on x [B][d] (and u [B][c] where the
  * method takes a control): drift/sigma/w/Z/V_true/u_true/V_grad_true/b_tf

@@ -1,0 +1,161 @@
+"""The fused NN-control rollout (dpac_rollout_nn_fwd: actor MLP on MFMA tiles inside
+the time loop, equation.py:46-106 + solver.py:260-278) against
+
+  * the float64 oracle's propagate_* with the oracle DeepNN as NN_control,
+  * the product's unfused path (PyTorch MLP between dpac_step_fwd launches),
+  * PyTorch's own layer outputs for the backward saves.
+
+Tolerances: float64 |a-b| <= 1e-10 (1+|b|) on x, dt, u (the MFMA and the GEMM
+library sum the 200-term dot products in different orders; ~1e-16 per step),
+coef exact; float32 vs the float64 oracle: <= 1e-3 of trajectories may flip an
+exit decision, matched trajectories within 1e-4 (1+|b|).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from deeppde_actorcritic_amd import _lib, ops
+from deeppde_actorcritic_amd import equation as peq
+from deeppde_actorcritic_amd import solver as psol
+from deeppde_actorcritic_amd.config import set_floatx
+from oracle import equations as oeq
+from oracle import solver as osol
+from tests.helpers import full_config, rel_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SCHEMES = {"naive": _lib.SCHEME_NAIVE, "adaptive": _lib.SCHEME_ADAPTIVE}
+
+
+def actor_pair(cfg, dtype):
+    """Product actor DeepNN (on the GPU, `dtype`) and the oracle DeepNN with the same weights."""
+    set_floatx("float64" if dtype == torch.float64 else "float32")
+    gen = torch.Generator().manual_seed(3)
+    net = psol.DeepNN(cfg, "actor", gen, dtype, DEV)
+    onet = osol.DeepNN(cfg, "actor", net.export_params())
+    return net, onet
+
+
+CASES = [("LQR", 20, (200, 200, 200)), ("LQR", 5, (16, 16)), ("VDP", 4, (50, 50)),
+         ("VDP", 10, (32, 48, 24)), ("EKN", 5, (40, 40)), ("EKN", 20, (64, 64, 64)),
+         ("LQR_var", 10, (200, 200, 200)), ("LQR_var", 5, (24,))]
+
+
+@pytest.mark.parametrize("name,d,hidden", CASES)
+@pytest.mark.parametrize("scheme", ["naive", "adaptive"])
+def test_fused_nn_rollout_vs_oracle_fp64(name, d, hidden, scheme):
+    B, N, T = 37, 20, 0.2  # 37: a partial last 16-row tile
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme=scheme)
+    eo = oeq.make(cfg.eqn_config)
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, onet = actor_pair(cfg, torch.float64)
+    np.random.seed(11)
+    x0, dw, _ = eo.sample_normal(B, N)
+    prop = eo.propagate_naive if scheme == "naive" else eo.propagate_adaptive
+    xr, dtr, cr = prop(B, x0, dw, onet, False, T, N, False)
+    x, dt, coef, u, _, _, _ = ops.rollout_nn(
+        ep.params(), SCHEMES[scheme], torch.as_tensor(x0, device=DEV),
+        torch.as_tensor(dw, device=DEV).permute(2, 0, 1).contiguous(), T, N, net.mlp_view())
+    np.testing.assert_array_equal(coef.cpu().numpy(), cr.numpy())
+    assert rel_close(x.permute(1, 2, 0).cpu(), xr, 1e-10)
+    assert rel_close(dt.cpu(), dtr, 1e-10)
+    # the control the kernel applied is the oracle MLP at the recorded states
+    ur = torch.stack([onet(xr[:, :, t], False, need_grad=False) for t in range(N)])
+    assert rel_close(u.cpu(), ur, 1e-10)
+
+
+@pytest.mark.parametrize("name,d,hidden", [("LQR", 20, (200, 200, 200)), ("EKN", 20, (64, 64, 64)),
+                                           ("VDP", 20, (200, 200, 200))])
+def test_fused_nn_rollout_fp32_vs_oracle(name, d, hidden):
+    B, N, T = 512, 50, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme="adaptive", dtype="float32")
+    eo = oeq.make(cfg.eqn_config)
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, onet = actor_pair(cfg, torch.float32)
+    np.random.seed(12)
+    x0, dw, _ = eo.sample_normal(B, N)
+    xr, dtr, cr = eo.propagate_adaptive(B, x0, dw, onet, False, T, N, False)
+    x, dt, coef, _, _, _, _ = ops.rollout_nn(
+        ep.params(), _lib.SCHEME_ADAPTIVE, torch.as_tensor(x0, dtype=torch.float32, device=DEV),
+        torch.as_tensor(dw, dtype=torch.float32, device=DEV).permute(2, 0, 1).contiguous(), T, N,
+        net.mlp_view())
+    same = np.all(coef.cpu().numpy() == cr.numpy(), axis=1)
+    assert np.mean(~same) <= 1e-3
+    assert rel_close(x.permute(1, 2, 0).cpu().double().numpy()[same], xr.numpy()[same], 1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_fused_matches_unfused_product_path(dtype):
+    """dpac_rollout_nn_fwd vs PyTorch MLP + dpac_step_fwd per step (rollout_nn_nograd)."""
+    name, d, B, N, T = "LQR", 20, 300, 40, 0.2
+    cfg = full_config(name, d, N=N, hidden=(200, 200, 200), scheme="adaptive")
+    ep = peq.LQR(cfg.eqn_config)
+    net, _ = actor_pair(cfg, dtype)
+    eqp = ep.params()
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=5, dtype=dtype, device=DEV)
+    xa, dta, ca, ua, _, _, _ = ops.rollout_nn(eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, net.mlp_view())
+    with torch.no_grad():
+        xb, dtb, cb, ub = peq.rollout_nn_nograd(eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, net)
+    tol = 1e-10 if dtype == torch.float64 else 2e-4
+    same = torch.all(ca == cb, dim=1).cpu().numpy()
+    assert np.mean(~same) <= (0 if dtype == torch.float64 else 1e-2)
+    assert rel_close(xa[:, same].cpu(), xb[:, same].cpu(), tol)
+    assert rel_close(ua[:, same].cpu(), ub[:, same].cpu(), tol)
+
+
+def test_backward_saves_and_cost():
+    """save_z holds every dense layer's pre-BN output; save_flag / save_disc the state
+    entering each step; y / disc equal the actor-cost kernel over the same path."""
+    name, d, B, N, T = "LQR", 5, 40, 12, 0.2
+    hidden = (24, 40)
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme="adaptive")
+    ep = peq.LQR(cfg.eqn_config)
+    net, _ = actor_pair(cfg, torch.float64)
+    eqp = ep.params()
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=6, dtype=torch.float64, device=DEV)
+    x, dt, coef, u, y, disc, (z, flag, disc_t) = ops.rollout_nn(
+        eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, net.mlp_view(), cost_order=_lib.COST_ACTOR, save=True)
+    # pre-BN layer outputs, recomputed with PyTorch from the recorded states
+    rs, g, bt, W = net.bn_rs, net.bn_gamma, net.bn_beta, net.W
+    with torch.no_grad():
+        a = torch.addcmul(bt[0], x[:N].reshape(-1, d), rs * g[0])
+        zs = []
+        for i in range(len(hidden)):
+            zi = a @ W[i]
+            zs.append(zi)
+            a = torch.addcmul(bt[i + 1], zi, rs * g[i + 1])
+            a = a + torch.relu(a)
+        zs.append(a @ W[-1])
+    assert rel_close(z.reshape(N * B, -1).cpu(), torch.cat(zs, 1).cpu(), 1e-12)
+    # flags / discount entering each step
+    yr, discr = ops.actor_cost(eqp, x, u, dt, coef)
+    assert rel_close(y.cpu(), yr.cpu(), 1e-12) and rel_close(disc.cpu(), discr.cpu(), 1e-12)
+    cum = torch.cumprod(torch.exp(-(dt * coef)), 1)  # gamma = 1
+    disc_ref = torch.cat([torch.ones(B, 1, dtype=cum.dtype, device=DEV), cum[:, :-1]], 1).t()
+    assert rel_close(disc_t.cpu(), disc_ref.cpu(), 1e-12)
+    f0 = ops.flag_init(eqp, _lib.SCHEME_ADAPTIVE, x0, T, N)
+    assert torch.equal(flag[0], f0)
+    alive = (flag > 0).to(coef.dtype)
+    assert torch.equal(alive[1:], coef.t()[:-1])  # alive after step t iff step t kept going
+
+
+def test_invalid_mlp_rejected():
+    cfg = full_config("LQR", 5, N=4, hidden=(16, 16))
+    ep = peq.LQR(cfg.eqn_config)
+    net, _ = actor_pair(cfg, torch.float64)
+    eqp = ep.params()
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, 8, 4, seed=1, dtype=torch.float64, device=DEV)
+    view = net.mlp_view()
+    view.struct.width[1] = 300  # wider than DPAC_MLP_MAX_WIDTH
+    with pytest.raises(_lib.DpacError):
+        ops.rollout_nn(eqp, _lib.SCHEME_NAIVE, x0, dw, 0.2, 4, view)
+    view = net.mlp_view()
+    view.struct.ekn_head = 1  # Eikonal head on LQR
+    with pytest.raises(_lib.DpacError):
+        ops.rollout_nn(eqp, _lib.SCHEME_NAIVE, x0, dw, 0.2, 4, view)
+    view = net.mlp_view()
+    view.struct.width[0] = 4  # input width != dim
+    with pytest.raises(_lib.DpacError):
+        ops.rollout_nn(eqp, _lib.SCHEME_NAIVE, x0, dw, 0.2, 4, view)
