@@ -148,9 +148,8 @@ class Equation(object):
                 x, disc, y, dt, coef, flag = ops.sde_step(eqp, sch, T, N, x, u, dw[t], flag, disc, y)
                 xs.append(x); us.append(u); dts.append(dt); coefs.append(coef)
             return torch.stack(xs), torch.stack(dts, 1), torch.stack(coefs, 1), torch.stack(us)
-        view = NN_control.mlp_view() if hasattr(NN_control, "mlp_view") else None
-        if view is not None and view.supported():  # one fused launch, MLP on MFMA
-            x, dt, coef, u, _, _, _ = ops.rollout_nn(eqp, sch, x0, dw, T, N, view)
+        if hasattr(NN_control, "fused_ok") and NN_control.fused_ok():  # one launch, MLP on MFMA
+            x, dt, coef, u, _, _, _ = ops.rollout_nn(eqp, sch, x0, dw, T, N, NN_control.mlp_view())
             return x, dt, coef, u
         return rollout_nn_nograd(eqp, sch, x0, dw, T, N, NN_control)
 

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -168,6 +169,102 @@ def rollout_nn(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor, total_time:
          _ptr(disc), _ptr(saves[0] if saves else None), _ptr(saves[1] if saves else None),
          _ptr(saves[2] if saves else None), _stream(x0))
     return x, dt, coef, u, y, disc, saves
+
+
+class _ActorRolloutNN(torch.autograd.Function):
+    """The actor's pathwise cost (solver.py:207-219) over a fused NN-control rollout,
+    differentiable in the actor's parameters (BPTT, what GradientTape does for
+    solver.py:92-97).
+
+    forward: one dpac_rollout_nn_fwd launch with the backward saves.
+    backward: a reverse time loop of dpac_step_bwd plus the MLP's input-gradient
+    chain (per layer one scaled multiply and one [B x w] @ [w x w'] product),
+    storing the gradient entering every BatchNorm output for all steps; the
+    parameter gradients are then a few products/reductions over all N*B rows.
+    Inputs: x0, dw, rs, then DeepNN.trainable_variables() (gamma[L+2], beta[L+2],
+    W[L+1], b).  Outputs: y [B], disc_N [B], x_N [B, d]."""
+
+    @staticmethod
+    def forward(ctx, x0, dw, rs, eqp, scheme, T, N, ekn, *params):
+        L = (len(params) - 1) // 3 - 1
+        gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
+        scales = [rs * g for g in gam]
+        view = MlpView(scales, bet, Ws, b, ekn)
+        x, dt, coef, u, y, disc, (z, flag, disc_t) = rollout_nn(
+            eqp, scheme, x0, dw, T, N, view, cost_order=_lib.COST_ACTOR, save=True)
+        ctx.save_for_backward(x, u, dw, z, flag, disc_t, rs, *params)
+        ctx.cfg = (eqp, scheme, T, N, ekn, L)
+        return y, disc, x[N].clone()
+
+    @staticmethod
+    def backward(ctx, g_y, g_disc, g_xN):
+        x, u, dw, z, flag, disc_t, rs, *params = ctx.saved_tensors
+        eqp, scheme, T, N, ekn, L = ctx.cfg
+        gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
+        B, d = x.shape[1], x.shape[2]
+        widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+        s = [rs * g for g in gam]
+        zoff = np.cumsum([0] + widths[1:]).tolist()
+        zl = [None] + [z[:, :, zoff[i - 1]:zoff[i]] for i in range(1, L + 2)]
+        # activation factors 1 + [y_l > 0] and post-activations a_l for all steps (l = 1..L)
+        fac, act = [None] * (L + 1), [None] * (L + 1)
+        for i in range(1, L + 1):
+            yl = torch.addcmul(bet[i], zl[i], s[i])
+            fac[i] = 1.0 + (yl > 0).to(yl.dtype)
+            act[i] = yl + torch.relu(yl)
+        Wss = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]  # (W diag(s))^T
+        G = [torch.empty(N, B, w, dtype=x.dtype, device=x.device) for w in widths]
+        kw = dict(dtype=x.dtype, device=x.device)
+        gx = torch.zeros(B, d, **kw) if g_xN is None else g_xN.contiguous()
+        gd = torch.zeros(B, **kw) if g_disc is None else g_disc.clone()  # ping-pong buffer below
+        gy = torch.zeros(B, **kw) if g_y is None else g_y.contiguous()
+        gx_dir, gu, gd_new = torch.empty_like(gx), torch.empty_like(u[0]), torch.empty_like(gd)
+        if ekn:
+            ob = torch.addcmul(bet[L + 1], zl[L + 1] + b, s[L + 1])  # BN_last output, all steps
+            c = widths[L + 1] - 1
+        for t in range(N - 1, -1, -1):
+            call("dpac_step_bwd", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
+                 _ptr(x[t]), _ptr(u[t]), _ptr(dw[t]), _ptr(flag[t]), _ptr(disc_t[t]),
+                 _lib.COST_ACTOR, _ptr(gx), _ptr(gd), _ptr(gy), _ptr(gx_dir), _ptr(gu),
+                 _ptr(gd_new), _stream(x))
+            if ekn:  # u = o[:c] / (1e-15 + relu(o_c) + |o[:c]|), solver.py:272-274
+                o = ob[t]
+                oc, oh = o[:, c], o[:, :c]
+                nrm = torch.sqrt(torch.sum(oh * oh, 1))
+                den = (1e-15 + torch.relu(oc)) + nrm
+                k = torch.sum(gu * oh, 1) / (den * den)
+                G[L + 1][t, :, :c] = gu / den[:, None] - (k / nrm)[:, None] * oh
+                G[L + 1][t, :, c] = -k * (oc > 0).to(o.dtype)
+            else:
+                G[L + 1][t].copy_(gu)
+            ga = G[L + 1][t] @ Wss[L]
+            for i in range(L, 0, -1):
+                torch.mul(ga, fac[i][t], out=G[i][t])
+                ga = G[i][t] @ Wss[i - 1]
+            G[0][t].copy_(ga)
+            gx = torch.addcmul(gx_dir, ga, s[0])
+            gd, gd_new = gd_new, gd
+        # parameter gradients over all N*B rows
+        rows = lambda tt: tt.reshape(N * B, -1)
+        zin = [x[:N]] + [zl[i] for i in range(1, L + 1)] + [zl[L + 1] + b]
+        dgam = [rs * torch.sum(rows(G[i] * zin[i]), 0) for i in range(L + 2)]
+        dbet = [torch.sum(rows(G[i]), 0) for i in range(L + 2)]
+        A = [torch.addcmul(bet[0], x[:N], s[0])] + [act[i] for i in range(1, L + 1)]
+        dW = [rows(A[i]).t() @ rows(G[i + 1] * s[i + 1]) for i in range(L + 1)]
+        db = torch.sum(rows(G[L + 1] * s[L + 1]), 0)
+        return (None, None, None, None, None, None, None, None, *dgam, *dbet, *dW, db)
+
+
+def actor_rollout_nn(eqp, scheme: int, x0, dw, total_time: float, num_steps: int, net):
+    """(y [B], disc_N [B], x_N [B,d]) of the actor's rollout with `net` (a DeepNN) as
+    control, differentiable in net's parameters through _ActorRolloutNN."""
+    if not torch.is_grad_enabled():  # evaluation only: no backward saves
+        x, _, _, _, y, disc, _ = rollout_nn(eqp, scheme, x0, dw, total_time, num_steps,
+                                            net.mlp_view(), want_u=False, cost_order=_lib.COST_ACTOR)
+        return y, disc, x[num_steps]
+    return _ActorRolloutNN.apply(x0.contiguous(), dw.contiguous(), net.bn_rs, eqp, scheme,
+                                 float(total_time), int(num_steps), bool(net.ekn_head),
+                                 *net.trainable_variables())
 
 
 def flag_init(eqp, scheme: int, x0: torch.Tensor, total_time: float, num_steps: int):

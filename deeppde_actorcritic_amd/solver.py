@@ -94,6 +94,10 @@ class DeepNN(nn.Module):
             y = y[:, 0:d] / (1e-15 + torch.relu(y[:, d:d + 1]) + norm_y)
         return y
 
+    def fused_ok(self) -> bool:
+        """Whether dpac_rollout_nn_fwd can run this network (layer and width limits)."""
+        return 1 <= len(self.sizes) - 2 <= _lib.MLP_MAX_HIDDEN and max(self.sizes) <= _lib.MLP_MAX_WIDTH
+
     @torch.no_grad()
     def mlp_view(self):
         """This network as dpac_rollout_nn_fwd reads it (BN scale = rs * gamma, the same
@@ -172,6 +176,9 @@ class ActorModel(nn.Module):
             x, _, _, _, y, disc = ops.rollout_analytic(eqp, self.scheme, x0, dw, T, N,
                                                        cost_order=_lib.COST_ACTOR)
             xN = x[N]
+        elif self.NN_control.fused_ok():
+            # fused NN rollout forward + manual BPTT backward (ops._ActorRolloutNN)
+            y, disc, xN = ops.actor_rollout_nn(eqp, self.scheme, x0, dw, T, N, self.NN_control)
         else:
             flag = ops.flag_init(eqp, self.scheme, x0, T, N)
             disc = torch.ones(B, dtype=x0.dtype, device=x0.device)
