@@ -13,7 +13,7 @@ HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
              -DDPAC_DIMS=$(DIMS) -DDPAC_DIMS_EVEN=$(DIMS_EVEN) -Wno-pass-failed \
              -ffp-contract=off
 EQNS      := lqr lqrvar ekn vdp
-HDRS      := $(CSRC)/dpac_device.h $(CSRC)/dpac_kernels.h include/dpac.h
+HDRS      := $(wildcard $(CSRC)/*.h) include/dpac.h
 OBJS      := $(OBJDIR)/dpac_abi.o \
              $(foreach e,$(EQNS),$(OBJDIR)/dpac_eqn_$(e)_f32.o $(OBJDIR)/dpac_eqn_$(e)_f64.o)
 LIB       := $(PKG)/libdpac.so

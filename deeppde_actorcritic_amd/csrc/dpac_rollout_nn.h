@@ -24,6 +24,12 @@ constexpr int kNnThreads = 256;  // 4 wavefronts
 constexpr int kNnWaves = kNnThreads / 64;
 constexpr int kNnLd = DPAC_MLP_MAX_WIDTH + 4;  // LDS row stride (elements)
 constexpr int kNnMaxTilesPerWave = (DPAC_MLP_MAX_WIDTH / 16 + kNnWaves - 1) / kNnWaves;
+constexpr int kNnPrefetch = 8;  // k-steps of B in flight per tile
+#ifndef DPAC_NN_ABLATE
+#define DPAC_NN_ABLATE 0  // timing-only builds: 1 = constant weights, 2 = skip the MLP
+#endif
+// The ring reads A up to k < 4 * roundup(ceil(K/4), kNnPrefetch) <= 256 for K <= 256.
+static_assert(DPAC_MLP_MAX_WIDTH <= 256 && kNnLd >= 256, "A reads stay inside an LDS row");
 
 // 16x16x4 MFMA for one precision.  A[row l&15][k l>>4], B[k l>>4][col l&15];
 // the accumulator's element i of lane l is C[row(l, i)][l&15].
@@ -70,59 +76,102 @@ struct NnRolloutArgs {
 
 // One dense layer for the workgroup's 16 rows: out = act(BN(in @ W (+ b))).
 // in/out are [16][kNnLd] LDS images; columns >= Nout of the last tile are
-// written as 0 so the next layer's K padding reads zeros.
-template <typename T>
-__device__ __forceinline__ void nn_layer(const T* in, T* out, int K, int Nout, const T* W,
-                                         const T* scale, const T* shift, const T* bias,
-                                         bool hidden, int wave, int lane, T* save_row0,
-                                         int64_t save_stride, int rows_live) {
+// written as 0 so the next layer's K padding reads zeros.  NT = this wave's
+// 16-column tiles (wave, wave + 4, ...): a template constant, so the K loop is
+// straight-line MFMA code with no per-tile predicate.
+template <typename T, int NT>
+__device__ __forceinline__ void nn_layer_tiles(const T* in, T* out, int K, int Nout, const T* W,
+                                               const T* scale, const T* shift, const T* bias,
+                                               bool hidden, int wave, int lane, T* save_row0,
+                                               int64_t save_stride, int rows_live) {
   using MF = Mfma<T>;
-  const int ntiles = (Nout + 15) / 16;
-  const int mine = ntiles > wave ? (ntiles - wave + kNnWaves - 1) / kNnWaves : 0;
   const int col_l = lane & 15, kq = lane >> 4;
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, (uint32_t)(K * Nout * (int)sizeof(T)));
-  uint32_t voff[kNnMaxTilesPerWave];
-  typename MF::acc_t acc[kNnMaxTilesPerWave];
+  uint32_t voff[NT];
+  typename MF::acc_t acc[NT];
+  T s[NT], sh[NT], bb[NT];
 #pragma unroll
-  for (int j = 0; j < kNnMaxTilesPerWave; ++j) {
+  for (int j = 0; j < NT; ++j) {
     const int col = (wave + kNnWaves * j) * 16 + col_l;
-    voff[j] = (j < mine && col < Nout) ? (uint32_t)((kq * Nout + col) * (int)sizeof(T)) : kOOB;
+    const bool valid = col < Nout;
+    voff[j] = valid ? (uint32_t)((kq * Nout + col) * (int)sizeof(T)) : kOOB;
     acc[j] = typename MF::acc_t{0, 0, 0, 0};
+    s[j] = valid ? scale[col] : T(0);  // epilogue constants, loaded before the K loop
+    sh[j] = valid ? shift[col] : T(0);
+    bb[j] = (valid && bias) ? bias[col] : T(0);
   }
   const uint32_t kstep_bytes = (uint32_t)(4 * Nout * (int)sizeof(T));
   const int nks = (K + 3) / 4;
   const T* arow = in + col_l * kNnLd + kq;  // A[row = lane&15][k = 4ks + lane>>4]
-#pragma unroll 4
-  for (int ks = 0; ks < nks; ++ks) {
-    const T a = arow[4 * ks];
+  // B comes from L2 (~0.5-1k cycles): a kNnPrefetch-deep ring of k-steps keeps that
+  // many loads per tile in flight.  Rows k >= K fall outside the descriptor and
+  // read 0, so the ring needs no predicate; A past K is LDS zero padding.
+  auto loadB = [&](int ks, int j) {
+#if DPAC_NN_ABLATE == 1
+    return T(1e-3) * T(j + 1) + T(ks & 1);  // timing only: no weight traffic
+#endif
+    uint32_t w[sizeof(T) / 4];
+    buf_load_dwords<sizeof(T) / 4>(rW, voff[j] + (uint32_t)ks * kstep_bytes, w);
+    T v;
+    __builtin_memcpy(&v, &w[0], sizeof(T));
+    return v;
+  };
+  // A (LDS) is read one ring iteration ahead too; k-steps past the last are
+  // clamped to it (their B is 0, so the product adds nothing).
+  auto loadA = [&](int ks) { return arow[4 * (ks < nks ? ks : nks - 1)]; };
+  T bq[kNnPrefetch][NT], av[kNnPrefetch];
 #pragma unroll
-    for (int j = 0; j < kNnMaxTilesPerWave; ++j) {
-      if (j < mine) {
-        uint32_t w[sizeof(T) / 4];
-        buf_load_dwords<sizeof(T) / 4>(rW, voff[j] + (uint32_t)ks * kstep_bytes, w);
-        T b;
-        __builtin_memcpy(&b, &w[0], sizeof(T));
-        acc[j] = MF::mma(a, b, acc[j]);
+  for (int q = 0; q < kNnPrefetch; ++q) {
+    av[q] = loadA(q);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bq[q][j] = loadB(q, j);
+  }
+  for (int ks0 = 0; ks0 < nks; ks0 += kNnPrefetch) {
+    T an[kNnPrefetch];
+#pragma unroll
+    for (int q = 0; q < kNnPrefetch; ++q) an[q] = loadA(ks0 + kNnPrefetch + q);
+#pragma unroll
+    for (int q = 0; q < kNnPrefetch; ++q) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        acc[j] = MF::mma(av[q], bq[q][j], acc[j]);
+        bq[q][j] = loadB(ks0 + q + kNnPrefetch, j);
       }
     }
+#pragma unroll
+    for (int q = 0; q < kNnPrefetch; ++q) av[q] = an[q];
   }
 #pragma unroll
-  for (int j = 0; j < kNnMaxTilesPerWave; ++j) {
-    if (j >= mine) continue;
+  for (int j = 0; j < NT; ++j) {
     const int col = (wave + kNnWaves * j) * 16 + col_l;
     const bool valid = col < Nout;
-    const T s = valid ? scale[col] : T(0), sh = valid ? shift[col] : T(0);
-    const T bb = (valid && bias) ? bias[col] : T(0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = MF::row(lane, i);
       const T z = acc[j][i];
       if (save_row0 && valid && row < rows_live) save_row0[row * save_stride + col] = z;
-      T yv = bias ? z + bb : z;           // addmm(b, y, W) (solver.py:270)
-      yv = sh + yv * s;                   // addcmul(beta, y, gamma/sqrt(1+eps))
-      if (hidden) yv = yv + fmax(yv, T(0));  // y + relu(y) (solver.py:269)
+      T yv = bias ? z + bb[j] : z;            // addmm(b, y, W) (solver.py:270)
+      yv = sh[j] + yv * s[j];                 // addcmul(beta, y, gamma/sqrt(1+eps))
+      if (hidden) yv = yv + fmax(yv, T(0));   // y + relu(y) (solver.py:269)
       out[row * kNnLd + col] = valid ? yv : T(0);
     }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void nn_layer(const T* in, T* out, int K, int Nout, const T* W,
+                                         const T* scale, const T* shift, const T* bias,
+                                         bool hidden, int wave, int lane, T* save_row0,
+                                         int64_t save_stride, int rows_live) {
+  const int ntiles = (Nout + 15) / 16;
+  const int mine = ntiles > wave ? (ntiles - wave + kNnWaves - 1) / kNnWaves : 0;  // wave-uniform
+  static_assert(kNnMaxTilesPerWave == 4, "dispatch below covers 1..4 tiles");
+  switch (mine) {
+    case 1: nn_layer_tiles<T, 1>(in, out, K, Nout, W, scale, shift, bias, hidden, wave, lane, save_row0, save_stride, rows_live); break;
+    case 2: nn_layer_tiles<T, 2>(in, out, K, Nout, W, scale, shift, bias, hidden, wave, lane, save_row0, save_stride, rows_live); break;
+    case 3: nn_layer_tiles<T, 3>(in, out, K, Nout, W, scale, shift, bias, hidden, wave, lane, save_row0, save_stride, rows_live); break;
+    case 4: nn_layer_tiles<T, 4>(in, out, K, Nout, W, scale, shift, bias, hidden, wave, lane, save_row0, save_stride, rows_live); break;
+    default: break;
   }
 }
 
@@ -154,7 +203,12 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
   const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(a.u, a.u ? slab_u * (uint32_t)a.N : 0u);
   const int L = mlp.L, c_out = mlp.width[L + 1];
 
-  for (int i = tid; i < kNnRows * kNnLd; i += kNnThreads) s_x0[i] = T(0);  // K padding
+  // zero padding: A columns past K (up to a prefetch ring beyond) read zeros
+  for (int i = tid; i < kNnRows * kNnLd; i += kNnThreads) {
+    s_x0[i] = T(0);
+    s_pq[0][i] = T(0);
+    s_pq[1][i] = T(0);
+  }
   // BN_0 coefficients of the owned components
   T s0[M], b0[M];
 #pragma unroll
@@ -186,7 +240,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
     // ---- actor MLP on MFMA (all four wavefronts) ----
     const T* in = s_x0;
     int pq = 0;
-    for (int l = 0; l <= L; ++l) {
+    for (int l = 0; l <= (DPAC_NN_ABLATE == 2 ? -1 : L); ++l) {  // ablation 2: no MLP (timing)
       T* out = s_pq[pq];
       T* save = a.save_z ? a.save_z + ((int64_t)t * a.B + row0) * mlp.ztot + mlp.zoff[l + 1] : nullptr;
       nn_layer<T>(in, out, mlp.width[l], mlp.width[l + 1], mlp.weight[l], mlp.scale[l + 1],

@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--seed", type=int, default=11, help="weight-initialisation seed")
     ap.add_argument("--data-seed", type=int, default=123, help="np.random.seed before train()")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "train_check.json"))
+    ap.add_argument("--oracle-from", default=None,
+                    help="reuse the oracle history of an earlier train_check JSON (same settings)")
     a = ap.parse_args()
     runs = a.runs.split(",")
     res = {"config": "lqr_d20 (configs/lqr_d20.json values)", "iters": a.iters, "log_freq": a.log_freq,
@@ -118,6 +120,10 @@ def main():
                                  "threads": torch.get_num_threads()}
         print(json.dumps({"run": "oracle", "wall_s": wall, "err_value": res["runs"]["oracle"]["history"]["err_value"]}),
               flush=True)
+    if a.oracle_from:
+        prev = json.load(open(a.oracle_from))
+        assert (prev["iters"], prev["log_freq"], prev["batch"], prev["valid"]) == (a.iters, a.log_freq, a.batch, a.valid)
+        res["runs"]["oracle"] = dict(prev["runs"]["oracle"], source=a.oracle_from)
     if "oracle" in res["runs"]:
         ref = np.array(res["runs"]["oracle"]["history"]["err_value"])
         res["max_abs_err_value_diff_vs_oracle"] = {
