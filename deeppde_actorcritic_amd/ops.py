@@ -250,7 +250,9 @@ class _ActorRolloutNN(torch.autograd.Function):
         dgam = [rs * torch.sum(rows(G[i] * zin[i]), 0) for i in range(L + 2)]
         dbet = [torch.sum(rows(G[i]), 0) for i in range(L + 2)]
         A = [torch.addcmul(bet[0], x[:N], s[0])] + [act[i] for i in range(1, L + 1)]
-        dW = [rows(A[i]).t() @ rows(G[i + 1] * s[i + 1]) for i in range(L + 1)]
+        # per-step partial products summed over N (split-K; one GEMM with an N*B-long
+        # reduction runs far below the MFMA rate)
+        dW = [torch.bmm(A[i].transpose(1, 2), G[i + 1] * s[i + 1]).sum(0) for i in range(L + 1)]
         db = torch.sum(rows(G[L + 1] * s[L + 1]), 0)
         return (None, None, None, None, None, None, None, None, *dgam, *dbet, *dW, db)
 

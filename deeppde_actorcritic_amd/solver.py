@@ -78,20 +78,30 @@ class DeepNN(nn.Module):
                              persistent=False)
 
     def forward(self, x, training=False, need_grad=False):
+        """x [rows, d], or [S, R, d] for a stack of S batches (e.g. the critic's G over
+        all N steps): then every product is a batched GEMM over S with the weight
+        broadcast, so autograd forms the weight gradients as S partial products and
+        a sum instead of one GEMM with a 10^5-long reduction."""
         rs = self.bn_rs
         g, bt, W = self.bn_gamma, self.bn_beta, self.W
         L = len(self.sizes) - 2
+        if x.dim() == 3:
+            S = x.shape[0]
+            mm = lambda a, w: torch.bmm(a, w.unsqueeze(0).expand(S, -1, -1))
+            mm_bias = lambda b, a, w: torch.baddbmm(b, a, w.unsqueeze(0).expand(S, -1, -1))
+        else:
+            mm, mm_bias = torch.mm, torch.addmm
         y = torch.addcmul(bt[0], x, rs * g[0])
         for i in range(L):
-            y = torch.mm(y, W[i])
+            y = mm(y, W[i])
             y = torch.addcmul(bt[i + 1], y, rs * g[i + 1])
             y = y + torch.relu(y)
-        y = torch.addmm(self.b, y, W[L])
+        y = mm_bias(self.b, y, W[L])
         y = torch.addcmul(bt[L + 1], y, rs * g[L + 1])
         if self.ekn_head:  # solver.py:272-274
             d = self.d
-            norm_y = torch.sum(y[:, 0:d] ** 2, 1, keepdim=True) ** 0.5
-            y = y[:, 0:d] / (1e-15 + torch.relu(y[:, d:d + 1]) + norm_y)
+            norm_y = torch.sum(y[..., 0:d] ** 2, -1, keepdim=True) ** 0.5
+            y = y[..., 0:d] / (1e-15 + torch.relu(y[..., d:d + 1]) + norm_y)
         return y
 
     def fused_ok(self) -> bool:
@@ -145,7 +155,7 @@ class CriticModel(nn.Module):
                                                model_actor.NN_control, cheat=cheat_control)
         G = None
         if self.td == _lib.TD1:
-            G = self.NN_value_grad(x[:N].reshape(N * B, d), training).reshape(N, B, d)
+            G = self.NN_value_grad(x[:N], training)  # [N, B, d], batched over the N steps
         y, disc = ops.td_assemble(self.bsde.params(), self.td, x, u, dw, dt, coef, G,
                                   cost_order=_lib.COST_CRITIC)
         V = self.NN_value(torch.cat([x[0], x[N], x_bdry]), training)[:, 0]
@@ -246,6 +256,34 @@ class TFAdam:
         return {"iterations": self.iterations}
 
 
+class _GradGraph:
+    """One gradient evaluation (forward + backward, no optimizer step) captured as a
+    HIP graph over static input buffers.  Replaying it after copying a fresh batch
+    in replaces the ~10^3 kernel launches of a step (the actor's reverse time loop,
+    the critic's G network and TD assembly) with one graph launch; the optimizer
+    still runs eagerly on the returned gradients, whose buffers the next replay
+    overwrites.  Parameters are updated in place, so every replay sees the
+    current weights."""
+
+    def __init__(self, fn, batch: TrajectoryBatch):
+        self.static = TrajectoryBatch(*[t.clone() for t in batch])
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up outside the capture (allocator, autograd)
+            for _ in range(2):
+                fn(self.static)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = fn(self.static)
+
+    def __call__(self, batch: TrajectoryBatch):
+        for dst, src in zip(self.static, batch):
+            dst.copy_(src)
+        self.graph.replay()
+        return list(self.out)
+
+
 def _huber_mean(delta):
     """solver.py:76-77 (quadratic inside |delta| < 50, linear outside)."""
     a = torch.abs(delta)
@@ -263,10 +301,13 @@ class ActorCriticSolver(object):
                   is unseeded, SURVEY.md quirk 2);
       sampler  -- "device" (rocRAND Philox on the GPU, default) or "host" (the
                   reference's numpy/scipy stream, bit-identical inputs);
-      parallel -- a parallel.DataParallel for multi-GPU data parallelism.
+      parallel -- a parallel.DataParallel for multi-GPU data parallelism;
+      graphs   -- capture each training step's gradient evaluation as a HIP graph
+                  (default: on with the device sampler; results are identical).
     """
 
-    def __init__(self, config, bsde, seed=None, sampler=None, parallel=None, device=None):
+    def __init__(self, config, bsde, seed=None, sampler=None, parallel=None, device=None,
+                 graphs=None):
         self.eqn_config = config.eqn_config
         self.net_config = config.net_config
         self.train_config = config.train_config
@@ -309,6 +350,8 @@ class ActorCriticSolver(object):
         else:
             raise ValueError(f"unknown train mode {self.train_config.train!r}")
         self._calls = 0
+        self.hip_graphs = (self.sampler == "device") if graphs is None else bool(graphs)
+        self._graphs = {}
         if self.sampler == "host":
             self._np_rng_state = None
 
@@ -354,15 +397,27 @@ class ActorCriticSolver(object):
     def _global(self, data, total):
         return data.x0.shape[0], total
 
+    def _grads(self, kind, fn, data):
+        """fn(batch) -> gradients, through a captured HIP graph when enabled."""
+        data = Equation.to_native(data, self.dtype)
+        if not self.hip_graphs:
+            return fn(data)
+        key = (kind, tuple(data.dw.shape))
+        graph = self._graphs.get(key)
+        if graph is None:
+            graph = self._graphs[key] = _GradGraph(fn, data)
+        return graph(data)
+
     def train_step_critic(self, train_data, total=None):
-        g = self.grad_critic(train_data, training=False, cheat_control=self.cheat_control_in_critic)
+        g = self._grads("critic", lambda d: self.grad_critic(
+            d, training=False, cheat_control=self.cheat_control_in_critic), train_data)
         cnt = train_data[0].shape[0]
         g = self.par.allreduce_grads(g, cnt, total or cnt * self.par.world)
         self.optimizer_critic.apply_gradients(zip(g, self.critic_variables()))
 
     def train_step_actor(self, train_data, total=None):
-        g = self.grad_actor(train_data, training=False, cheat_value=self.cheat_value_in_actor,
-                            cheat_control=False)
+        g = self._grads("actor", lambda d: self.grad_actor(
+            d, training=False, cheat_value=self.cheat_value_in_actor, cheat_control=False), train_data)
         cnt = train_data[0].shape[0]
         g = self.par.allreduce_grads(g, cnt, total or cnt * self.par.world)
         self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))

@@ -113,3 +113,19 @@ def test_reference_layout_propagate_surface():
         assert tuple(xs.shape) == (16, 5, 11) and tuple(dt.shape) == (16, 10)
         assert rel_close(xs.cpu(), xr, 1e-12) and rel_close(dt.cpu(), dtr, 1e-12)
         assert np.array_equal(coef.cpu().numpy(), cr.numpy())
+
+
+@pytest.mark.parametrize("name,d,td", [("LQR", 20, "TD1"), ("EKN", 5, "TD2"), ("VDP", 4, "TD1")])
+def test_hip_graph_steps_match_eager(name, d, td):
+    """Training steps replayed from captured HIP graphs give the parameters of eager steps."""
+    cfg = full_config(name, d, N=10, hidden=(32, 32), batch=64, valid=64, td=td)
+    res = []
+    for graphs in (False, True):
+        bp = getattr(peq, name)(cfg.eqn_config)
+        sp = psol.ActorCriticSolver(cfg, bp, seed=7, sampler="device", graphs=graphs)
+        for _ in range(3):
+            sp.train_step_critic(sp.sample(64, 10))
+            sp.train_step_actor(sp.sample(64, 10))
+        res.append([v.detach().cpu() for v in sp.critic_variables() + sp.actor_variables()])
+    for a, b in zip(*res):
+        assert rel_close(a, b, 1e-12)
