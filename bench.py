@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 METRIC = "SDE trajectory-steps/sec (batch×horizon) at d=20; value-fn rel-L2 vs analytic"
 B_PER_GPU, DIM, HORIZON, T_TOTAL = 4096, 20, 200, 0.2
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
+MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
 BYTES_PER_TRAJ_STEP_F32 = (2 * DIM + 2) * 4  # read dw[d] + write x[d] + dt + coef
 
 
@@ -68,6 +69,29 @@ def time_launches(launch, steps, warmup, world):
     wall = time.perf_counter() - t0
     per_launch_ms = start.elapsed_time(end) / steps
     return wall, per_launch_ms
+
+
+def training_iteration(dtype, iters=8, warmup=3):
+    """End-to-end lqr_d20 training iteration (critic step + actor step, solver.py:67-70)
+    on on-device samples, the reference's shape: B=2048, N=100, 3x200 MLPs, TD1."""
+    from deeppde_actorcritic_amd import equation as peq
+    from deeppde_actorcritic_amd import solver as psol
+    from tools.train_check import lqr_d20
+    cfg = lqr_d20(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", 2048, 2048)
+    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=1, sampler="device")
+    B, N = 2048, cfg.eqn_config.num_time_interval_critic
+    for _ in range(warmup):
+        sp.train_step_critic(sp.sample(B, N))
+        sp.train_step_actor(sp.sample(B, N))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        sp.train_step_critic(sp.sample(B, N))
+        sp.train_step_actor(sp.sample(B, N))
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / iters * 1e3
+    return {"ms_per_iteration": ms, "batch": B, "horizon": N, "mlp": "20-200-200-200-20",
+            "note": "critic + actor step, HIP-graph replay, fused NN rollouts"}
 
 
 def max_over_ranks(v, world):
@@ -123,6 +147,7 @@ def main():
     ap.add_argument("--scheme", choices=["adaptive", "naive"], default="adaptive")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--no-train", action="store_true", help="skip the training-iteration variant")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,6 +238,28 @@ def main():
         variants["td1_assembly"] = {
             "traj_steps_per_s": world * B * N * k3 / max_over_ranks(wall3, world), "avg_launch_ms": pl3,
             "hbm_GBps_algorithmic": B * N * (3 * d + d + 2) * esize / (pl3 * 1e-3) / 1e9}
+        # fused NN-control rollout: actor MLP d-200-200-200-d on MFMA inside the time loop
+        from deeppde_actorcritic_amd import solver as psol
+        from tools.train_check import lqr_d20
+        cfg_nn = lqr_d20(1, 1, "float32" if dtype == torch.float32 else "float64", B, B)
+        net = psol.DeepNN(cfg_nn, "actor", torch.Generator().manual_seed(0), dtype, "cuda")
+        view = net.mlp_view()
+        nn_out = {}
+
+        def nn_launch():
+            nn_out["r"] = ops.rollout_nn(eqp, scheme, x0, dw, T_TOTAL, N, view, want_u=False)
+        k4 = max(5, args.steps // 20)
+        wall4, pl4 = time_launches(nn_launch, k4, 2, world)
+        widths = [d, 200, 200, 200, d]
+        flops = 2 * sum(widths[i] * widths[i + 1] for i in range(4)) * B * N
+        tfs = flops / (pl4 * 1e-3) / 1e12
+        variants["rollout_nn_fused"] = {
+            "traj_steps_per_s": world * B * N * k4 / max_over_ranks(wall4, world), "avg_launch_ms": pl4,
+            "mlp": "-".join(map(str, widths)),
+            "roofline": {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "dpac::k_rollout_nn"}}
+        if world == 1 and not args.no_train:
+            variants["training_lqr_d20"] = training_iteration(dtype)
         out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
