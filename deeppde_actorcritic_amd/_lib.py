@@ -89,6 +89,9 @@ SIGNATURES = {
     "dpac_equation_eval": [_EQ, _I32, _I32, _I64, _P, _P, _P, _P],
     "dpac_rollout_nn_fwd": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp), _P, _P, _P, _P,
                             _P, _P, _I32, _P, _P, _P, _P, _P, _P],
+    "dpac_rollout_nn_bwd": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp),
+                            ctypes.POINTER(ctypes.c_void_p), _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                            _P, _P, _P],
 }
 _RESTYPES = {"dpac_abi_version": ctypes.c_int32, "dpac_last_error": ctypes.c_char_p,
              "dpac_supported": ctypes.c_int32}

@@ -95,6 +95,33 @@ int check_sample_type(int32_t st) {
   return DPAC_OK;
 }
 
+int check_mlp(const dpac_eqn_params* eq, const dpac_mlp* actor) {
+  if (!actor) return fail(DPAC_EINVAL, "actor MLP pointer is NULL");
+  const int L = actor->n_hidden;
+  if (L < 1 || L > DPAC_MLP_MAX_HIDDEN)
+    return fail(DPAC_EINVAL, "actor: n_hidden must be in [1, %d] (got %d)", DPAC_MLP_MAX_HIDDEN, L);
+  if (actor->ekn_head != 0 && actor->ekn_head != 1)
+    return fail(DPAC_EINVAL, "actor: ekn_head must be 0 or 1");
+  if (actor->ekn_head && eq->eqn != DPAC_EQN_EKN)
+    return fail(DPAC_EINVAL, "actor: the Eikonal head applies to the EKN equation only");
+  for (int i = 0; i <= L + 1; ++i) {
+    if (actor->width[i] < 1 || actor->width[i] > DPAC_MLP_MAX_WIDTH)
+      return fail(DPAC_EINVAL, "actor: width[%d] = %d outside [1, %d]", i, actor->width[i],
+                  DPAC_MLP_MAX_WIDTH);
+    if (!actor->bn_scale[i] || !actor->bn_shift[i])
+      return fail(DPAC_EINVAL, "actor: bn_scale/bn_shift[%d] is NULL", i);
+    if (i <= L && !actor->weight[i]) return fail(DPAC_EINVAL, "actor: weight[%d] is NULL", i);
+  }
+  if (!actor->bias) return fail(DPAC_EINVAL, "actor: bias is NULL");
+  if (actor->width[0] != eq->dim)
+    return fail(DPAC_EINVAL, "actor: width[0] (%d) must equal dim (%d)", actor->width[0], eq->dim);
+  if (actor->width[L + 1] != eq->control_dim + actor->ekn_head)
+    return fail(DPAC_EINVAL, "actor: output width %d must be control_dim%s (%d)",
+                actor->width[L + 1], actor->ekn_head ? " + 1" : "",
+                eq->control_dim + actor->ekn_head);
+  return DPAC_OK;
+}
+
 #define DPAC_REQUIRE(ptr) \
   if (!(ptr)) return fail(DPAC_EINVAL, "%s: required pointer '%s' is NULL", __func__, #ptr)
 
@@ -309,34 +336,12 @@ int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
                         void* stream) {
   if (int e = check_common(eq, dtype, num_sample)) return e;
   if (int e = check_time(scheme, num_steps, total_time)) return e;
-  DPAC_REQUIRE(actor);
+  if (int e = check_mlp(eq, actor)) return e;
   DPAC_REQUIRE(x0);
   DPAC_REQUIRE(dw);
   DPAC_REQUIRE(x);
   DPAC_REQUIRE(dt);
   DPAC_REQUIRE(coef);
-  const int L = actor->n_hidden;
-  if (L < 1 || L > DPAC_MLP_MAX_HIDDEN)
-    return fail(DPAC_EINVAL, "actor: n_hidden must be in [1, %d] (got %d)", DPAC_MLP_MAX_HIDDEN, L);
-  if (actor->ekn_head != 0 && actor->ekn_head != 1)
-    return fail(DPAC_EINVAL, "actor: ekn_head must be 0 or 1");
-  if (actor->ekn_head && eq->eqn != DPAC_EQN_EKN)
-    return fail(DPAC_EINVAL, "actor: the Eikonal head applies to the EKN equation only");
-  for (int i = 0; i <= L + 1; ++i) {
-    if (actor->width[i] < 1 || actor->width[i] > DPAC_MLP_MAX_WIDTH)
-      return fail(DPAC_EINVAL, "actor: width[%d] = %d outside [1, %d]", i, actor->width[i],
-                  DPAC_MLP_MAX_WIDTH);
-    if (!actor->bn_scale[i] || !actor->bn_shift[i])
-      return fail(DPAC_EINVAL, "actor: bn_scale/bn_shift[%d] is NULL", i);
-    if (i <= L && !actor->weight[i]) return fail(DPAC_EINVAL, "actor: weight[%d] is NULL", i);
-  }
-  if (!actor->bias) return fail(DPAC_EINVAL, "actor: bias is NULL");
-  if (actor->width[0] != eq->dim)
-    return fail(DPAC_EINVAL, "actor: width[0] (%d) must equal dim (%d)", actor->width[0], eq->dim);
-  if (actor->width[L + 1] != eq->control_dim + actor->ekn_head)
-    return fail(DPAC_EINVAL, "actor: output width %d must be control_dim%s (%d)",
-                actor->width[L + 1], actor->ekn_head ? " + 1" : "",
-                eq->control_dim + actor->ekn_head);
   if ((y == nullptr) != (disc == nullptr))
     return fail(DPAC_EINVAL, "y and disc must both be given or both be NULL");
   if (cost_order != DPAC_COST_CRITIC && cost_order != DPAC_COST_ACTOR)
@@ -349,6 +354,37 @@ int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
   a.x0 = x0; a.dw = dw; a.mlp = *actor;
   a.x_out = x; a.dt = dt; a.coef = coef; a.u_out = u; a.cost_order = cost_order; a.y = y;
   a.disc = disc; a.save_z = save_z; a.save_flag = save_flag; a.save_disc = save_disc;
+  a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                        int64_t num_sample, int32_t num_steps, double total_time,
+                        const dpac_mlp* actor, const void* const* weight_t, const void* x,
+                        const void* u, const void* dw, const void* save_z,
+                        const int32_t* save_flag, const void* save_disc, const void* g_xN,
+                        const void* g_disc, const void* g_y, void* G, void* g_x0,
+                        void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (int e = check_time(scheme, num_steps, total_time)) return e;
+  if (int e = check_mlp(eq, actor)) return e;
+  DPAC_REQUIRE(weight_t);
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(u);
+  DPAC_REQUIRE(dw);
+  DPAC_REQUIRE(save_z);
+  DPAC_REQUIRE(save_flag);
+  DPAC_REQUIRE(save_disc);
+  DPAC_REQUIRE(G);
+  for (int i = 0; i <= actor->n_hidden; ++i)
+    if (!weight_t[i]) return fail(DPAC_EINVAL, "weight_t[%d] is NULL", i);
+  OpArgs a = blank(eq, OP_ROLLOUT_NN_BWD);
+  a.scheme = scheme; a.dtype = dtype; a.B = num_sample; a.N = num_steps; a.T = total_time;
+  a.mlp = *actor;
+  for (int i = 0; i <= actor->n_hidden; ++i) a.mlp_wt[i] = weight_t[i];
+  a.x = x; a.u = u; a.dw = dw; a.save_z = const_cast<void*>(save_z);
+  a.save_flag = const_cast<int32_t*>(save_flag); a.save_disc = const_cast<void*>(save_disc);
+  a.g_x_out = g_xN; a.g_disc_out = g_disc; a.g_y_out = g_y; a.g_G = G; a.g_x = g_x0;
   a.stream = (hipStream_t)stream;
   return launch(a);
 }

@@ -31,6 +31,7 @@ enum Op : int {
   OP_TD_BWD,
   OP_EVAL,
   OP_ROLLOUT_NN,
+  OP_ROLLOUT_NN_BWD,
 };
 
 // Everything any op may need; unused fields are ignored.
@@ -51,6 +52,7 @@ struct OpArgs {
   dpac_mlp mlp;                  // OP_ROLLOUT_NN: the actor MLP
   void *save_z, *save_disc;      // OP_ROLLOUT_NN: optional backward saves
   int32_t* save_flag;
+  const void* mlp_wt[DPAC_MLP_MAX_HIDDEN + 1];  // OP_ROLLOUT_NN_BWD: (W_i diag s_{i+1})^T
   hipStream_t stream;
 };
 
@@ -485,25 +487,16 @@ __global__ __launch_bounds__(64) void k_step_fwd(const E eq, const DevConsts<T> 
 //   dL/du    = c*dt*lam·∂f/∂u + c*sqrt(dt)*(lam⊙dw)·∂s/∂u + g_y'*c*dt*disc*∂w/∂u
 //   dL/dx    = lam + (same three terms w.r.t. x) + dL/ddt * ∂dt/∂x
 //   ∂dt/∂x   = -2(R-r)x/(r*den) if flag == 1 and dt_raw >= 1e-4 dt0 (TF max tie rule), else 0
-template <typename T, class E, int D, int SCHEME>
-__global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> c,
-                                                  const StepArgs<T> a) {
+// The VJP of one transition for the owned slice (shared by k_step_bwd and the
+// fused reverse rollout).  lam = dL/dx', gD1 = dL/ddisc', gy1 = dL/dy'.
+template <typename T, class E, int SCHEME>
+__device__ __forceinline__ void step_vjp(const E& eq, const DevConsts<T>& c, const T (&x)[E::M],
+                                         const T (&u)[E::MC], const T (&dw)[E::M], Flags fl,
+                                         T disc, const T (&lam)[E::M], T gD1, T gy1,
+                                         T (&gx)[E::M], T (&gu)[E::MC], T& g_disc) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
   using TR = Transition<T, E, SCHEME>;
-  const LaneCoord<P> lc(a.B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
-  const Own<D, P> own(lc.p);
-  const Own<E::CDIM, P> ownu(lc.p);
-  T x[M], u[MC], dw[M], lam[M];
-  own.load_masked(a.x + lc.b * D, x);
-  own.load_masked(a.dw + lc.b * D, dw);
-  own.load_masked(a.g_x_out + lc.b * D, lam);
-  ownu.load_masked(a.u + lc.b * E::CDIM, u);
   const T r = dsqrt(Lanes<P>::sum(sumsq(x)));
-  const Flags fl = Flags::decode(a.flag_in[lc.b]);
-  const T disc = a.disc_in ? a.disc_in[lc.b] : T(1);
-  const T gD1 = a.g_disc_out ? a.g_disc_out[lc.b] : T(0);
-  const T gy1 = a.g_y_out ? a.g_y_out[lc.b] : T(0);
-
   TR tr;
   tr.run(eq, c, x, u, dw, fl, r);
   const T cf = tr.coef ? T(1) : T(0);
@@ -513,7 +506,7 @@ __global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> 
   T f[M], s[M];
   eq.drift(x, u, r, f);
   eq.sigma(x, u, s);
-  T gx[M], gu[MC], a_f[M], a_s[M];
+  T a_f[M], a_s[M];
   T part = 0;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -528,7 +521,7 @@ __global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> 
   eq.sigma_vjp(x, u, a_s, gx, gu);
   const T gw = gy1 * cf * tr.dt * disc;
   eq.w_vjp(x, u, gw, gx, gu);
-  const T g_disc = gD1 * Ef + gy1 * cf * w * tr.dt;
+  g_disc = gD1 * Ef + gy1 * cf * w * tr.dt;
   if constexpr (SCHEME == DPAC_SCHEME_ADAPTIVE) {
     const T g_dt = gD1 * disc * Ef * (c.neg_gamma * cf) + gy1 * cf * w * disc + cf * Lanes<P>::sum(part);
     const T raw = adaptive_dt_raw(fl.layer, r, c);
@@ -538,6 +531,26 @@ __global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> 
       for (int m = 0; m < M; ++m) gx[m] += k * x[m];
     }
   }
+}
+
+template <typename T, class E, int D, int SCHEME>
+__global__ __launch_bounds__(64) void k_step_bwd(const E eq, const DevConsts<T> c,
+                                                  const StepArgs<T> a) {
+  constexpr int P = E::kP, M = E::M, MC = E::MC;
+  const LaneCoord<P> lc(a.B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
+  const Own<D, P> own(lc.p);
+  const Own<E::CDIM, P> ownu(lc.p);
+  T x[M], u[MC], dw[M], lam[M];
+  own.load_masked(a.x + lc.b * D, x);
+  own.load_masked(a.dw + lc.b * D, dw);
+  own.load_masked(a.g_x_out + lc.b * D, lam);
+  ownu.load_masked(a.u + lc.b * E::CDIM, u);
+  const Flags fl = Flags::decode(a.flag_in[lc.b]);
+  const T disc = a.disc_in ? a.disc_in[lc.b] : T(1);
+  const T gD1 = a.g_disc_out ? a.g_disc_out[lc.b] : T(0);
+  const T gy1 = a.g_y_out ? a.g_y_out[lc.b] : T(0);
+  T gx[M], gu[MC], g_disc;
+  step_vjp<T, E, SCHEME>(eq, c, x, u, dw, fl, disc, lam, gD1, gy1, gx, gu, g_disc);
   own.store(a.g_x + lc.b * D, gx);
   ownu.store(a.g_u + lc.b * E::CDIM, gu);
   if (a.g_disc && lc.p == 0) a.g_disc[lc.b] = g_disc;
@@ -740,6 +753,26 @@ __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, i
 // ---------------------------------------------------------------------------
 // Launcher for one (T, equation functor, D).
 // ---------------------------------------------------------------------------
+// The kernel-side view of a dpac_mlp (column offsets of each layer's saved z).
+template <typename T>
+NnMlp<T> nn_mlp(const dpac_mlp& h) {
+  NnMlp<T> m{};
+  m.L = h.n_hidden;
+  m.ekn = h.ekn_head;
+  int z = 0;
+  for (int i = 0; i <= m.L + 1; ++i) {
+    m.width[i] = h.width[i];
+    m.scale[i] = (const T*)h.bn_scale[i];
+    m.shift[i] = (const T*)h.bn_shift[i];
+    m.zoff[i] = i == 0 ? 0 : z;
+    if (i > 0) z += m.width[i];
+  }
+  m.ztot = z;
+  for (int i = 0; i <= m.L; ++i) m.weight[i] = (const T*)h.weight[i];
+  m.bias = (const T*)h.bias;
+  return m;
+}
+
 inline dim3 grid_for(int64_t B, int P) {
   const int64_t per = 64 / P;
   return dim3((unsigned)((B + per - 1) / per));
@@ -836,6 +869,26 @@ int run_op(const OpArgs& a) {
       hipLaunchKernelGGL((k_eval<T, E, D>), grid, block, 0, s, eq, c, a.B, a.what,
                          (const T*)a.x, (const T*)a.u, (T*)a.out);
       break;
+    case OP_ROLLOUT_NN_BWD: {
+      NnMlp<T> m = nn_mlp<T>(a.mlp);
+      NnBackArgs<T> r{};
+      r.B = a.B; r.N = a.N;
+      r.x = (const T*)a.x; r.u = (const T*)a.u; r.dw = (const T*)a.dw;
+      r.disc_t = (const T*)a.save_disc; r.z = (const T*)a.save_z; r.flag = a.save_flag;
+      r.g_xN = (const T*)a.g_x_out; r.g_disc = (const T*)a.g_disc_out; r.g_y = (const T*)a.g_y_out;
+      r.G = (T*)a.g_G; r.g_x0 = (T*)a.g_x;
+      int go = 0;
+      for (int i = 0; i <= m.L + 1; ++i) {
+        r.goff[i] = go;
+        go += m.width[i];
+      }
+      r.gtot = go;
+      for (int i = 0; i <= m.L; ++i) r.wt[i] = (const T*)a.mlp_wt[i];
+      const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
+      if (adaptive) hipLaunchKernelGGL((k_rollout_nn_bwd<T, E, D, DPAC_SCHEME_ADAPTIVE>), ngrid, nblock, 0, s, eq, c, m, r);
+      else hipLaunchKernelGGL((k_rollout_nn_bwd<T, E, D, DPAC_SCHEME_NAIVE>), ngrid, nblock, 0, s, eq, c, m, r);
+      break;
+    }
     case OP_ROLLOUT_NN: {
       NnMlp<T> m{};
       m.L = a.mlp.n_hidden;

@@ -74,38 +74,37 @@ struct NnRolloutArgs {
   int32_t* save_flag;
 };
 
-// One dense layer for the workgroup's 16 rows: out = act(BN(in @ W (+ b))).
-// in/out are [16][kNnLd] LDS images; columns >= Nout of the last tile are
-// written as 0 so the next layer's K padding reads zeros.  NT = this wave's
-// 16-column tiles (wave, wave + 4, ...): a template constant, so the K loop is
-// straight-line MFMA code with no per-tile predicate.
-template <typename T, int NT>
-__device__ __forceinline__ void nn_layer_tiles(const T* in, T* out, int K, int Nout, const T* W,
-                                               const T* scale, const T* shift, const T* bias,
-                                               bool hidden, int wave, int lane, T* save_row0,
-                                               int64_t save_stride, int rows_live) {
+// out[16 x Nout] = in[16 x K] @ W[K x Nout] for the workgroup's 16 rows, this
+// wave's NT 16-column tiles (wave, wave + 4, ...), followed by a per-element
+// epilogue.  `in` is a [16][kNnLd] LDS image whose columns >= K are zero; W is
+// row-major in global memory (L2-resident).  NT is a template constant, so the
+// K loop is straight-line MFMA code with no per-tile predicate.
+//   EPI::Col load(col, valid)                       per-column constants (before the K loop)
+//   void store(i, row, col, valid, acc, const Col&) one output element (i: accumulator slot)
+template <typename T, int NT, class EPI>
+__device__ __forceinline__ void mfma_rows16(const T* in, int K, int Nout, const T* W, int wave,
+                                            int lane, EPI& epi) {
   using MF = Mfma<T>;
   const int col_l = lane & 15, kq = lane >> 4;
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, (uint32_t)(K * Nout * (int)sizeof(T)));
   uint32_t voff[NT];
   typename MF::acc_t acc[NT];
-  T s[NT], sh[NT], bb[NT];
+  typename EPI::Col cc[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = (wave + kNnWaves * j) * 16 + col_l;
     const bool valid = col < Nout;
     voff[j] = valid ? (uint32_t)((kq * Nout + col) * (int)sizeof(T)) : kOOB;
     acc[j] = typename MF::acc_t{0, 0, 0, 0};
-    s[j] = valid ? scale[col] : T(0);  // epilogue constants, loaded before the K loop
-    sh[j] = valid ? shift[col] : T(0);
-    bb[j] = (valid && bias) ? bias[col] : T(0);
+    cc[j] = epi.load(col, valid);  // issued before the K loop: its latency hides there
   }
   const uint32_t kstep_bytes = (uint32_t)(4 * Nout * (int)sizeof(T));
   const int nks = (K + 3) / 4;
   const T* arow = in + col_l * kNnLd + kq;  // A[row = lane&15][k = 4ks + lane>>4]
   // B comes from L2 (~0.5-1k cycles): a kNnPrefetch-deep ring of k-steps keeps that
   // many loads per tile in flight.  Rows k >= K fall outside the descriptor and
-  // read 0, so the ring needs no predicate; A past K is LDS zero padding.
+  // read 0, so the ring needs no predicate.  A is read one ring iteration ahead;
+  // k-steps past the last are clamped to it (their B is 0, the product adds nothing).
   auto loadB = [&](int ks, int j) {
 #if DPAC_NN_ABLATE == 1
     return T(1e-3) * T(j + 1) + T(ks & 1);  // timing only: no weight traffic
@@ -116,8 +115,6 @@ __device__ __forceinline__ void nn_layer_tiles(const T* in, T* out, int K, int N
     __builtin_memcpy(&v, &w[0], sizeof(T));
     return v;
   };
-  // A (LDS) is read one ring iteration ahead too; k-steps past the last are
-  // clamped to it (their B is 0, so the product adds nothing).
   auto loadA = [&](int ks) { return arow[4 * (ks < nks ? ks : nks - 1)]; };
   T bq[kNnPrefetch][NT], av[kNnPrefetch];
 #pragma unroll
@@ -144,35 +141,212 @@ __device__ __forceinline__ void nn_layer_tiles(const T* in, T* out, int K, int N
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = (wave + kNnWaves * j) * 16 + col_l;
-    const bool valid = col < Nout;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = MF::row(lane, i);
-      const T z = acc[j][i];
-      if (save_row0 && valid && row < rows_live) save_row0[row * save_stride + col] = z;
-      T yv = bias ? z + bb[j] : z;            // addmm(b, y, W) (solver.py:270)
-      yv = sh[j] + yv * s[j];                 // addcmul(beta, y, gamma/sqrt(1+eps))
-      if (hidden) yv = yv + fmax(yv, T(0));   // y + relu(y) (solver.py:269)
-      out[row * kNnLd + col] = valid ? yv : T(0);
-    }
+    for (int i = 0; i < 4; ++i) epi.store(i, MF::row(lane, i), col, col < Nout, acc[j][i], cc[j]);
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void nn_layer(const T* in, T* out, int K, int Nout, const T* W,
-                                         const T* scale, const T* shift, const T* bias,
-                                         bool hidden, int wave, int lane, T* save_row0,
-                                         int64_t save_stride, int rows_live) {
+// Run mfma_rows16 with this wave's (wave-uniform) tile count.
+template <typename T, class EPI>
+__device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T* W, int wave,
+                                           int lane, EPI& epi) {
   const int ntiles = (Nout + 15) / 16;
-  const int mine = ntiles > wave ? (ntiles - wave + kNnWaves - 1) / kNnWaves : 0;  // wave-uniform
+  const int mine = ntiles > wave ? (ntiles - wave + kNnWaves - 1) / kNnWaves : 0;
   static_assert(kNnMaxTilesPerWave == 4, "dispatch below covers 1..4 tiles");
   switch (mine) {
-    case 1: nn_layer_tiles<T, 1>(in, out, K, Nout, W, scale, shift, bias, hidden, wave, lane, save_row0, save_stride, rows_live); break;
-    case 2: nn_layer_tiles<T, 2>(in, out, K, Nout, W, scale, shift, bias, hidden, wave, lane, save_row0, save_stride, rows_live); break;
-    case 3: nn_layer_tiles<T, 3>(in, out, K, Nout, W, scale, shift, bias, hidden, wave, lane, save_row0, save_stride, rows_live); break;
-    case 4: nn_layer_tiles<T, 4>(in, out, K, Nout, W, scale, shift, bias, hidden, wave, lane, save_row0, save_stride, rows_live); break;
+    case 1: mfma_rows16<T, 1>(in, K, Nout, W, wave, lane, epi); break;
+    case 2: mfma_rows16<T, 2>(in, K, Nout, W, wave, lane, epi); break;
+    case 3: mfma_rows16<T, 3>(in, K, Nout, W, wave, lane, epi); break;
+    case 4: mfma_rows16<T, 4>(in, K, Nout, W, wave, lane, epi); break;
     default: break;
   }
+}
+
+// Forward epilogue of a dense layer: z -> (save z) -> BN(z (+ b)) -> [y + relu(y)]
+// into the next layer's LDS input.  Padding columns are written as 0.
+template <typename T>
+struct FwdEpi {
+  struct Col {
+    T s, sh, bb;
+  };
+  const T *scale, *shift, *bias;
+  bool hidden;
+  T* out;          // LDS [16][kNnLd]
+  T* save;         // global row block of this layer's z, or null
+  int64_t save_stride;
+  int rows_live;
+  __device__ Col load(int col, bool valid) const {
+    return Col{valid ? scale[col] : T(0), valid ? shift[col] : T(0),
+               (valid && bias) ? bias[col] : T(0)};
+  }
+  __device__ void store(int, int row, int col, bool valid, T z, const Col& k) const {
+    if (save && valid && row < rows_live) save[row * save_stride + col] = z;
+    T yv = bias ? z + k.bb : z;          // addmm(b, y, W) (solver.py:270)
+    yv = k.sh + yv * k.s;                // addcmul(beta, y, gamma/sqrt(1+eps))
+    if (hidden) yv = yv + fmax(yv, T(0));  // y + relu(y) (solver.py:269)
+    out[row * kNnLd + col] = valid ? yv : T(0);
+  }
+};
+
+// Backward epilogue of a dense layer's input-gradient product g = G_{l+1} @ (W_l diag s_{l+1})^T:
+// for l >= 1 multiply by the activation factor 1 + [y_l > 0] of the forward step
+// (y_l = BN_l(z_l), z_l saved by the forward), then store the gradient entering
+// BN_l's output to global (the parameter gradients use it) and to LDS (the next
+// product's A).  l == 0 (no factor): the gradient entering a_0 = BN_0(x).
+template <typename T>
+struct BwdEpi {
+  struct Col {
+    T s, sh, z[4];
+  };
+  const T *scale, *shift;  // BN_l, or null for l == 0
+  const T* z;              // z_l of row 0 of the workgroup at this step
+  int64_t z_stride;
+  int rows_live, lane;
+  T* out;                  // LDS [16][kNnLd]
+  T* g;                    // G_l of row 0 of the workgroup at this step
+  int64_t g_stride;
+  __device__ Col load(int col, bool valid) const {
+    Col k{};
+    if (scale) {
+      k.s = valid ? scale[col] : T(0);
+      k.sh = valid ? shift[col] : T(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = Mfma<T>::row(lane, i);
+        k.z[i] = (valid && row < rows_live) ? z[row * z_stride + col] : T(0);
+      }
+    }
+    return k;
+  }
+  __device__ void store(int i, int row, int col, bool valid, T acc, const Col& k) const {
+    T v = acc;
+    if (scale) {
+      const T yv = k.sh + k.z[i] * k.s;  // the forward's BN_l output, same expression
+      v = acc * (yv > T(0) ? T(2) : T(1));  // d(y + relu(y))/dy
+    }
+    if (valid && row < rows_live) g[row * g_stride + col] = v;
+    out[row * kNnLd + col] = valid ? v : T(0);
+  }
+};
+
+template <typename T>
+struct NnBackArgs {
+  int64_t B;
+  int N;
+  const T *x, *u, *dw, *disc_t, *z;
+  const int32_t* flag;
+  const T *g_xN, *g_disc, *g_y;
+  T *G, *g_x0;
+  const T* wt[DPAC_MLP_MAX_HIDDEN + 1];  // (W_i diag s_{i+1})^T, [width[i+1]][width[i]]
+  int goff[DPAC_MLP_MAX_HIDDEN + 2];     // column offset of G_i in a G row
+  int gtot;
+};
+
+// The actor's BPTT through a fused NN rollout, as one launch: the reverse time
+// loop of step_vjp (the adjoint of the transition and the running cost) and the
+// MLP's input-gradient chain on MFMA, writing the gradient entering every BN
+// output of every step (G) for the parameter gradients.  Same workgroup layout
+// as k_rollout_nn.
+template <typename T, class E, int D, int SCHEME>
+__global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd(const E eq, const DevConsts<T> c,
+                                                              const NnMlp<T> mlp,
+                                                              const NnBackArgs<T> a) {
+  constexpr int P = E::kP, M = E::M, MC = E::MC, CD = E::CDIM;
+  __shared__ T s_pq[2][kNnRows * kNnLd];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
+  const int64_t row0 = (int64_t)blockIdx.x * kNnRows;
+  const int rows_live = (int)((a.B - row0) < kNnRows ? (a.B - row0) : kNnRows);
+  const bool stepper = tid < kNnRows * P;
+  const int g = stepper ? tid / P : 0;
+  const LaneCoord<P> lc(a.B, stepper ? tid % P : 0, row0 + g);
+  const bool live = stepper && lc.live;
+  const Own<D, P> own(lc.p);
+  const Own<CD, P> ownu(lc.p);
+  const int L = mlp.L;
+  for (int i = tid; i < kNnRows * kNnLd; i += kNnThreads) {
+    s_pq[0][i] = T(0);
+    s_pq[1][i] = T(0);
+  }
+  T s0[M], lam[M], gxd[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    s0[m] = own.valid(m) ? mlp.scale[0][own.j(m)] : T(0);
+    lam[m] = T(0);
+    gxd[m] = T(0);
+  }
+  if (a.g_xN) own.load_masked(a.g_xN + lc.b * D, lam);
+  T gD = a.g_disc ? a.g_disc[lc.b] : T(0);
+  const T gy = a.g_y ? a.g_y[lc.b] : T(0);
+  const T* sL = mlp.scale[L + 1];
+  const T* shL = mlp.shift[L + 1];
+  __syncthreads();
+  for (int t = a.N - 1; t >= 0; --t) {
+    const int64_t rowt = (int64_t)t * a.B;
+    if (stepper) {
+      T x[M], u[MC], dwv[M], gu[MC], gdn;
+      own.load_masked(a.x + (rowt + lc.b) * D, x);
+      own.load_masked(a.dw + (rowt + lc.b) * D, dwv);
+      ownu.load_masked(a.u + (rowt + lc.b) * CD, u);
+      const Flags fl = Flags::decode(a.flag[rowt + lc.b]);
+      step_vjp<T, E, SCHEME>(eq, c, x, u, dwv, fl, a.disc_t[rowt + lc.b], lam, gD, gy, gxd, gu, gdn);
+      gD = gdn;
+      // gradient at the network output, through the Eikonal head (solver.py:272-274)
+      T* grow = a.G + (rowt + lc.b) * a.gtot + a.goff[L + 1];
+      T* lrow = s_pq[0] + g * kNnLd;
+      if (mlp.ekn) {
+        const T* zr = a.z + (rowt + lc.b) * mlp.ztot + mlp.zoff[L + 1];
+        T o[MC];
+#pragma unroll
+        for (int m = 0; m < MC; ++m) {
+          const int j = ownu.j(m);
+          o[m] = ownu.valid(m) ? shL[j] + (zr[j] + mlp.bias[j]) * sL[j] : T(0);
+        }
+        const T oc = shL[CD] + (zr[CD] + mlp.bias[CD]) * sL[CD];
+        const T nrm = dsqrt(Lanes<P>::sum(sumsq(o)));
+        const T den = (T(1e-15) + fmax(oc, T(0))) + nrm;
+        T dot = 0;
+#pragma unroll
+        for (int m = 0; m < MC; ++m) dot += gu[m] * o[m];
+        const T k = Lanes<P>::sum(dot) / (den * den);
+#pragma unroll
+        for (int m = 0; m < MC; ++m) gu[m] = gu[m] / den - (k / nrm) * o[m];
+        if (lc.p == 0) {
+          const T goc = oc > T(0) ? -k : T(0);
+          lrow[CD] = goc;
+          if (live) grow[CD] = goc;
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MC; ++m) {
+        if (ownu.valid(m)) {
+          lrow[ownu.j(m)] = gu[m];
+          if (live) grow[ownu.j(m)] = gu[m];
+        }
+      }
+    }
+    __syncthreads();
+    // ---- input-gradient chain through the MLP (all four wavefronts) ----
+    const T* in = s_pq[0];
+    int pq = 1;
+    for (int l = L; l >= 0; --l) {
+      T* out = s_pq[pq];
+      BwdEpi<T> epi{l >= 1 ? mlp.scale[l] : nullptr, l >= 1 ? mlp.shift[l] : nullptr,
+                    a.z + (rowt + row0) * mlp.ztot + mlp.zoff[l], mlp.ztot, rows_live, lane, out,
+                    a.G + (rowt + row0) * a.gtot + a.goff[l], a.gtot};
+      mfma_layer<T>(in, mlp.width[l + 1], mlp.width[l], a.wt[l], wave, lane, epi);
+      __syncthreads();
+      in = out;
+      pq ^= 1;
+    }
+    if (stepper) {  // dL/dx_t = direct part + G_0 * s_0 (a_0 = beta_0 + x * s_0)
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        lam[m] = gxd[m] + (own.valid(m) ? in[g * kNnLd + own.j(m)] * s0[m] : T(0));
+    }
+    __syncthreads();
+  }
+  if (a.g_x0 && live) own.store(a.g_x0 + lc.b * D, lam);
 }
 
 template <typename T, class E, int D, int SCHEME, bool COST, int KB>
@@ -242,10 +416,10 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
     int pq = 0;
     for (int l = 0; l <= (DPAC_NN_ABLATE == 2 ? -1 : L); ++l) {  // ablation 2: no MLP (timing)
       T* out = s_pq[pq];
-      T* save = a.save_z ? a.save_z + ((int64_t)t * a.B + row0) * mlp.ztot + mlp.zoff[l + 1] : nullptr;
-      nn_layer<T>(in, out, mlp.width[l], mlp.width[l + 1], mlp.weight[l], mlp.scale[l + 1],
-                  mlp.shift[l + 1], l == L ? mlp.bias : nullptr, l < L, wave, lane, save, mlp.ztot,
-                  rows_live);
+      FwdEpi<T> epi{mlp.scale[l + 1], mlp.shift[l + 1], l == L ? mlp.bias : nullptr, l < L, out,
+                    a.save_z ? a.save_z + ((int64_t)t * a.B + row0) * mlp.ztot + mlp.zoff[l + 1] : nullptr,
+                    mlp.ztot, rows_live};
+      mfma_layer<T>(in, mlp.width[l], mlp.width[l + 1], mlp.weight[l], wave, lane, epi);
       __syncthreads();
       in = out;
       pq ^= 1;

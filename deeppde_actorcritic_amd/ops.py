@@ -206,55 +206,93 @@ class _ActorRolloutNN(torch.autograd.Function):
         s = [rs * g for g in gam]
         zoff = np.cumsum([0] + widths[1:]).tolist()
         zl = [None] + [z[:, :, zoff[i - 1]:zoff[i]] for i in range(1, L + 2)]
-        # activation factors 1 + [y_l > 0] and post-activations a_l for all steps (l = 1..L)
-        fac, act = [None] * (L + 1), [None] * (L + 1)
-        for i in range(1, L + 1):
-            yl = torch.addcmul(bet[i], zl[i], s[i])
-            fac[i] = 1.0 + (yl > 0).to(yl.dtype)
-            act[i] = yl + torch.relu(yl)
-        Wss = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]  # (W diag(s))^T
-        G = [torch.empty(N, B, w, dtype=x.dtype, device=x.device) for w in widths]
-        kw = dict(dtype=x.dtype, device=x.device)
-        gx = torch.zeros(B, d, **kw) if g_xN is None else g_xN.contiguous()
-        gd = torch.zeros(B, **kw) if g_disc is None else g_disc.clone()  # ping-pong buffer below
-        gy = torch.zeros(B, **kw) if g_y is None else g_y.contiguous()
-        gx_dir, gu, gd_new = torch.empty_like(gx), torch.empty_like(u[0]), torch.empty_like(gd)
-        if ekn:
-            ob = torch.addcmul(bet[L + 1], zl[L + 1] + b, s[L + 1])  # BN_last output, all steps
-            c = widths[L + 1] - 1
-        for t in range(N - 1, -1, -1):
-            call("dpac_step_bwd", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
-                 _ptr(x[t]), _ptr(u[t]), _ptr(dw[t]), _ptr(flag[t]), _ptr(disc_t[t]),
-                 _lib.COST_ACTOR, _ptr(gx), _ptr(gd), _ptr(gy), _ptr(gx_dir), _ptr(gu),
-                 _ptr(gd_new), _stream(x))
-            if ekn:  # u = o[:c] / (1e-15 + relu(o_c) + |o[:c]|), solver.py:272-274
-                o = ob[t]
-                oc, oh = o[:, c], o[:, :c]
-                nrm = torch.sqrt(torch.sum(oh * oh, 1))
-                den = (1e-15 + torch.relu(oc)) + nrm
-                k = torch.sum(gu * oh, 1) / (den * den)
-                G[L + 1][t, :, :c] = gu / den[:, None] - (k / nrm)[:, None] * oh
-                G[L + 1][t, :, c] = -k * (oc > 0).to(o.dtype)
-            else:
-                G[L + 1][t].copy_(gu)
-            ga = G[L + 1][t] @ Wss[L]
-            for i in range(L, 0, -1):
-                torch.mul(ga, fac[i][t], out=G[i][t])
-                ga = G[i][t] @ Wss[i - 1]
-            G[0][t].copy_(ga)
-            gx = torch.addcmul(gx_dir, ga, s[0])
-            gd, gd_new = gd_new, gd
+        gx_in = None if g_xN is None else g_xN.contiguous()
+        gd_in = None if g_disc is None else g_disc.contiguous()
+        gy_in = None if g_y is None else g_y.contiguous()
+        if BPTT_MODE == "fused":
+            G = _bptt_fused(eqp, scheme, T, N, ekn, L, x, u, dw, z, flag, disc_t, s, bet, Ws, b,
+                            widths, gx_in, gd_in, gy_in)
+        else:
+            G = _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b,
+                           widths, gx_in, gd_in, gy_in)
         # parameter gradients over all N*B rows
         rows = lambda tt: tt.reshape(N * B, -1)
         zin = [x[:N]] + [zl[i] for i in range(1, L + 1)] + [zl[L + 1] + b]
         dgam = [rs * torch.sum(rows(G[i] * zin[i]), 0) for i in range(L + 2)]
         dbet = [torch.sum(rows(G[i]), 0) for i in range(L + 2)]
-        A = [torch.addcmul(bet[0], x[:N], s[0])] + [act[i] for i in range(1, L + 1)]
+        A = [torch.addcmul(bet[0], x[:N], s[0])]
+        for i in range(1, L + 1):
+            yl = torch.addcmul(bet[i], zl[i], s[i])
+            A.append(yl + torch.relu(yl))
         # per-step partial products summed over N (split-K; one GEMM with an N*B-long
         # reduction runs far below the MFMA rate)
         dW = [torch.bmm(A[i].transpose(1, 2), G[i + 1] * s[i + 1]).sum(0) for i in range(L + 1)]
         db = torch.sum(rows(G[L + 1] * s[L + 1]), 0)
         return (None, None, None, None, None, None, None, None, *dgam, *dbet, *dW, db)
+
+
+# "fused": the reverse time loop as one dpac_rollout_nn_bwd launch; "loop": the
+# reference implementation of the same loop, dpac_step_bwd + PyTorch per step.
+BPTT_MODE = "fused"
+
+
+def _bptt_fused(eqp, scheme, T, N, ekn, L, x, u, dw, z, flag, disc_t, s, bet, Ws, b, widths,
+                g_xN, g_disc, g_y):
+    """G[i] = dL/d(output of BN_i) for every step, [N, B, width[i]], from one launch."""
+    B = x.shape[1]
+    view = MlpView(s, bet, Ws, b, ekn)
+    wt = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]
+    wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
+    goff = np.cumsum([0] + widths).tolist()
+    Gall = torch.empty(N, B, goff[-1], dtype=x.dtype, device=x.device)
+    call("dpac_rollout_nn_bwd", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
+         ctypes.byref(view.struct), wt_ptrs, _ptr(x), _ptr(u), _ptr(dw), _ptr(z), _ptr(flag),
+         _ptr(disc_t), _ptr(g_xN), _ptr(g_disc), _ptr(g_y), _ptr(Gall), None, _stream(x))
+    return [Gall[:, :, goff[i]:goff[i + 1]] for i in range(L + 2)]
+
+
+def _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b, widths,
+               g_xN, g_disc, g_y):
+    """The same G as _bptt_fused, step by step: dpac_step_bwd + the MLP's input-gradient
+    chain in PyTorch (per layer one scaled multiply and one [B x w] @ [w x w'] product)."""
+    B, d = x.shape[1], x.shape[2]
+    kw = dict(dtype=x.dtype, device=x.device)
+    fac = [None] * (L + 1)
+    for i in range(1, L + 1):
+        yl = torch.addcmul(bet[i], zl[i], s[i])
+        fac[i] = 1.0 + (yl > 0).to(yl.dtype)
+    Wss = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]  # (W diag(s))^T
+    G = [torch.empty(N, B, w, **kw) for w in widths]
+    gx = torch.zeros(B, d, **kw) if g_xN is None else g_xN
+    gd = torch.zeros(B, **kw) if g_disc is None else g_disc.clone()  # ping-pong buffer below
+    gy = torch.zeros(B, **kw) if g_y is None else g_y
+    gx_dir, gu, gd_new = torch.empty_like(gx), torch.empty(B, u.shape[2], **kw), torch.empty_like(gd)
+    if ekn:
+        ob = torch.addcmul(bet[L + 1], zl[L + 1] + b, s[L + 1])  # BN_last output, all steps
+        c = widths[L + 1] - 1
+    for t in range(N - 1, -1, -1):
+        call("dpac_step_bwd", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
+             _ptr(x[t]), _ptr(u[t]), _ptr(dw[t]), _ptr(flag[t]), _ptr(disc_t[t]),
+             _lib.COST_ACTOR, _ptr(gx), _ptr(gd), _ptr(gy), _ptr(gx_dir), _ptr(gu),
+             _ptr(gd_new), _stream(x))
+        if ekn:  # u = o[:c] / (1e-15 + relu(o_c) + |o[:c]|), solver.py:272-274
+            o = ob[t]
+            oc, oh = o[:, c], o[:, :c]
+            nrm = torch.sqrt(torch.sum(oh * oh, 1))
+            den = (1e-15 + torch.relu(oc)) + nrm
+            k = torch.sum(gu * oh, 1) / (den * den)
+            G[L + 1][t, :, :c] = gu / den[:, None] - (k / nrm)[:, None] * oh
+            G[L + 1][t, :, c] = -k * (oc > 0).to(o.dtype)
+        else:
+            G[L + 1][t].copy_(gu)
+        ga = G[L + 1][t] @ Wss[L]
+        for i in range(L, 0, -1):
+            torch.mul(ga, fac[i][t], out=G[i][t])
+            ga = G[i][t] @ Wss[i - 1]
+        G[0][t].copy_(ga)
+        gx = torch.addcmul(gx_dir, ga, s[0])
+        gd, gd_new = gd_new, gd
+    return G
 
 
 def actor_rollout_nn(eqp, scheme: int, x0, dw, total_time: float, num_steps: int, net):

@@ -254,6 +254,23 @@ int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
                         void* disc, void* save_z, int32_t* save_flag, void* save_disc,
                         void* stream);
 
+/* The actor's BPTT through a dpac_rollout_nn_fwd rollout (what GradientTape does
+ * for solver.py:92-97), as one launch.  Inputs: the forward's x, u, dw and its
+ * saves; `weight_t[i]` = (weight[i] * bn_scale[i+1])^T, [width[i+1]][width[i]]
+ * row-major, i = 0..n_hidden; the upstream gradients g_xN [B][d] (dL/dx_N),
+ * g_disc [B] (dL/d disc_N) and g_y [B] (dL/dy, the actor-order cost), each
+ * optional (NULL = 0).  Output G [N][B][Σ_i width[i]]: block i (column offset
+ * Σ_{k<i} width[k]) is dL/d(output of BN_i) at step t — for i = 0 the gradient
+ * entering a_0 = BN_0(x_t); for i = n_hidden+1 the network output before the
+ * Eikonal head.  The parameter gradients follow from G, the saved z and x by
+ * products over the N*B rows.  g_x0 [B][d] (optional): dL/dx_0. */
+int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                        int64_t num_sample, int32_t num_steps, double total_time,
+                        const dpac_mlp* actor, const void* const* weight_t, const void* x,
+                        const void* u, const void* dw, const void* save_z,
+                        const int32_t* save_flag, const void* save_disc, const void* g_xN,
+                        const void* g_disc, const void* g_y, void* G, void* g_x0, void* stream);
+
 /* ---- device equation coefficients (for parity tests and metrics) -------
  * Evaluates one Equation method row-wise on x [B][d] (and u [B][c] where the
  * method takes a control): drift/sigma/w/Z/V_true/u_true/V_grad_true/b_tf

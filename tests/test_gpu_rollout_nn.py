@@ -159,3 +159,29 @@ def test_invalid_mlp_rejected():
     view.struct.width[0] = 4  # input width != dim
     with pytest.raises(_lib.DpacError):
         ops.rollout_nn(eqp, _lib.SCHEME_NAIVE, x0, dw, 0.2, 4, view)
+
+
+@pytest.mark.parametrize("name,d,hidden,scheme", [
+    ("LQR", 20, (200, 200, 200), "adaptive"), ("LQR", 5, (24, 40), "naive"),
+    ("EKN", 5, (40, 40), "adaptive"), ("EKN", 20, (64, 64, 64), "naive"),
+    ("VDP", 4, (50, 50), "adaptive"), ("LQR_var", 10, (32, 48, 24), "adaptive")])
+def test_fused_bptt_kernel_matches_step_loop(name, d, hidden, scheme):
+    """dpac_rollout_nn_bwd (one launch) gives the parameter gradients of the per-step
+    reference loop (dpac_step_bwd + PyTorch MLP chain), float64, 1e-10."""
+    B, N, T = 37, 12, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme=scheme)
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, _ = actor_pair(cfg, torch.float64)
+    eqp = ep.params()
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=21, dtype=torch.float64, device=DEV)
+    grads = {}
+    try:
+        for mode in ("loop", "fused"):
+            ops.BPTT_MODE = mode
+            y, disc, xN = ops.actor_rollout_nn(eqp, SCHEMES[scheme], x0, dw, T, N, net)
+            loss = torch.mean(y + disc * torch.sum(xN * xN, 1))  # a smooth terminal value
+            grads[mode] = torch.autograd.grad(loss, net.trainable_variables())
+    finally:
+        ops.BPTT_MODE = "fused"
+    for a, b in zip(grads["fused"], grads["loop"]):
+        assert rel_close(a.cpu(), b.cpu(), 1e-10)
