@@ -238,6 +238,33 @@ __device__ __forceinline__ double row_pair_sum(double v) {
   return a + b;
 }
 
+// Shift register inside each lane group: lane p takes lane p-1's `keep`, the
+// group's first lane takes `v`.  One v_mov_dpp row_shr:1 whose source-less lane
+// (lane 0 of each 16-lane row) keeps `old` = v; groups shorter than a row also
+// select v on their first lane.
+template <int P, typename T>
+__device__ __forceinline__ T group_shift_in(T keep, T v, bool group_start) {
+  if constexpr (P == 1) {
+    return v;
+  } else {
+    constexpr int kRowShr1 = 0x111;
+    T sh;
+    if constexpr (sizeof(T) == 4) {
+      sh = __builtin_bit_cast(T, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v),
+                                                            __builtin_bit_cast(int, keep),
+                                                            kRowShr1, 0xF, 0xF, false));
+    } else {
+      const long long vb = __builtin_bit_cast(long long, v), kb = __builtin_bit_cast(long long, keep);
+      const int lo = __builtin_amdgcn_update_dpp((int)vb, (int)kb, kRowShr1, 0xF, 0xF, false);
+      const int hi = __builtin_amdgcn_update_dpp((int)(vb >> 32), (int)(kb >> 32), kRowShr1, 0xF, 0xF,
+                                                 false);
+      sh = __builtin_bit_cast(T, ((long long)hi << 32) | (unsigned int)lo);
+    }
+    if constexpr (P < 16) sh = group_start ? v : sh;
+    return sh;
+  }
+}
+
 template <int P>
 struct Lanes {
   static_assert(P == 1 || P == 2 || P == 4 || P == 8 || P == 16 || P == 32, "bad group size");

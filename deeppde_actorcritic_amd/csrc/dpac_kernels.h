@@ -322,9 +322,10 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
   constexpr int P = E::kP, M = E::M, MC = E::MC;
   constexpr bool COST = (OUT & kOutCost) != 0, WANT_U = (OUT & kOutU) != 0;
   // dt / coef rows are trajectory-major [B][N] (the reference's dt[B,N]): lane
-  // p of a group keeps step p of every F-step segment and the group writes the
-  // segment's F values of its row at once (F divides the pipeline period 2*KB,
-  // so each unrolled body knows its slot at compile time).
+  // group keeps its last F steps in a lane shift register (lane p: step t - p,
+  // dt with the sign of coef) and writes the F values of its row at once every
+  // F steps (F divides the pipeline period 2*KB, so each unrolled body knows at
+  // compile time whether it flushes).
   constexpr int F = P < 2 * KB ? P : 2 * KB;
   using TR = Transition<T, E, SCHEME>;
   const LaneCoord<P> lc(a.B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
@@ -341,12 +342,12 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
   const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(a.u, WANT_U ? slab_u * (uint32_t)a.N : 0u);
   const __amdgpu_buffer_rsrc_t rs_dt = make_rsrc(a.dt, (uint32_t)a.B * row_bytes);
   const __amdgpu_buffer_rsrc_t rs_cf = make_rsrc(a.coef, (uint32_t)a.B * row_bytes);
-  const uint32_t off_row = lc.live ? (uint32_t)(lc.b * row_bytes + lc.p * sizeof(T)) : kOOB;
-  T dt_keep = 0, cf_keep = 0;
-  auto flush = [&](int seg, int count) {  // steps [seg, seg + count) of the row
-    const uint32_t off = lc.p < count ? off_row : kOOB;
-    buf_store_scalar<T>(rs_dt, off, dt_keep, (uint32_t)seg * (uint32_t)sizeof(T));
-    buf_store_scalar<T>(rs_cf, off, cf_keep, (uint32_t)seg * (uint32_t)sizeof(T));
+  T keep = 0;  // coef_t ? dt_t : -dt_t (dt > 0 always) of step t_last - p
+  auto flush = [&](int t_last, int count) {  // steps (t_last - count, t_last] of the row
+    const uint32_t off = (lc.live && lc.p < count)
+                             ? (uint32_t)((lc.b * a.N + t_last - lc.p) * (int64_t)sizeof(T)) : kOOB;
+    buf_store_scalar<T>(rs_dt, off, fabs(keep));
+    buf_store_scalar<T>(rs_cf, off, keep > T(0) ? T(1) : T(0));
   };
 
   T x[M];
@@ -394,20 +395,18 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
     if constexpr (WANT_U) su.store(rs_u, u, (uint32_t)t * slab_u);
     if constexpr (DPAC_ABLATE != 3) {
       constexpr int PH = decltype(phase)::value;
-      const int slot = PH >= 0 ? PH % F : (t & (F - 1));
-      dt_keep = lc.p == slot ? tr.dt : dt_keep;
-      cf_keep = lc.p == slot ? cf : cf_keep;
+      keep = group_shift_in<P>(keep, tr.coef ? tr.dt : -tr.dt, lc.p == 0);
       if constexpr (PH >= 0) {
-        if constexpr (PH % F == F - 1) flush(t - (F - 1), F);
-      } else if (slot == F - 1) {
-        flush(t - (F - 1), F);
+        if constexpr (PH % F == F - 1) flush(t, F);
+      } else if ((t & (F - 1)) == F - 1) {
+        flush(t, F);
       }
     }
   };
   pipelined<KB, DwFrame<T, M>>(0, a.N, load, body);
   if constexpr (DPAC_ABLATE != 3 && DPAC_ABLATE != 1 && DPAC_ABLATE != 5) {
     const int rem = a.N & (F - 1);
-    if (rem) flush(a.N - rem, rem);
+    if (rem) flush(a.N - 1, rem);
   }
   if constexpr (COST) {
     if (lc.live && lc.p == 0) {

@@ -27,12 +27,24 @@ from deeppde_actorcritic_amd import solver as psol  # noqa: E402
 from deeppde_actorcritic_amd.config import munchify  # noqa: E402
 
 
-def lqr_d20(iters, log_freq, dtype, batch, valid):
+# eqn_config of the reference's BASELINE configs (configs/*.json values restated)
+EQN_CONFIGS = {
+    "lqr_d20": {"_comment": "linear quadratic regulator", "eqn_name": "LQR", "dim": 20, "control_dim": 20,
+                "discount": 1.0, "p": 1.0, "q": 1.0, "beta": 1.0, "R": 1.0},
+    "ekn_d20": {"_comment": "Diffusive Eikonal equation", "eqn_name": "EKN", "dim": 20, "control_dim": 20,
+                "discount": 0, "a2": 1.2, "a3": 0.2, "R": 1.0},
+    "lqr_var_d20": {"_comment": "linear quadratic regulator", "eqn_name": "LQR_var", "dim": 20,
+                    "control_dim": 20, "discount": 1.0, "q": 1.0, "beta": 1.0, "epsilon": 0.01, "R": 1.0},
+    "vdp_d20": {"_comment": "Van Der Pol oscillator", "eqn_name": "VDP", "dim": 20, "control_dim": 10,
+                "discount": 1.0, "a": 1.0, "epsilon": 0.1, "q": 1.0, "R": 1.0},
+}
+
+
+def lqr_d20(iters, log_freq, dtype, batch, valid, name="lqr_d20"):
+    eqn = dict(EQN_CONFIGS[name], total_time_critic=0.2, total_time_actor=0.2,
+               num_time_interval_critic=100, num_time_interval_actor=100)
     return munchify({
-        "eqn_config": {"_comment": "linear quadratic regulator", "eqn_name": "LQR",
-                       "total_time_critic": 0.2, "total_time_actor": 0.2, "dim": 20, "control_dim": 20,
-                       "num_time_interval_critic": 100, "num_time_interval_actor": 100,
-                       "discount": 1.0, "p": 1.0, "q": 1.0, "beta": 1.0, "R": 1.0},
+        "eqn_config": eqn,
         "net_config": {"num_hiddens_critic": [200, 200, 200], "num_hiddens_actor": [200, 200, 200],
                        "lr_values_critic": [1e-3, 1e-4, 1e-5], "lr_boundaries_critic": [30000, 40000],
                        "lr_values_actor": [1e-3, 1e-4, 1e-5], "lr_boundaries_actor": [30000, 40000],
@@ -72,6 +84,7 @@ def main():
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--valid", type=int, default=2048)
     ap.add_argument("--runs", default="gpu32,gpu64,oracle")
+    ap.add_argument("--config", default="lqr_d20", choices=sorted(EQN_CONFIGS))
     ap.add_argument("--seed", type=int, default=11, help="weight-initialisation seed")
     ap.add_argument("--data-seed", type=int, default=123, help="np.random.seed before train()")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "train_check.json"))
@@ -79,15 +92,15 @@ def main():
                     help="reuse the oracle history of an earlier train_check JSON (same settings)")
     a = ap.parse_args()
     runs = a.runs.split(",")
-    res = {"config": "lqr_d20 (configs/lqr_d20.json values)", "iters": a.iters, "log_freq": a.log_freq,
+    res = {"config": f"{a.config} (configs/{a.config}.json values)", "iters": a.iters, "log_freq": a.log_freq,
            "batch": a.batch, "valid": a.valid, "runs": {}}
     init = None
     for run in runs:
         if run == "oracle":
             continue
         dtype = "float32" if run == "gpu32" else "float64"
-        cfg = lqr_d20(a.iters, a.log_freq, dtype, a.batch, a.valid)
-        bsde = peq.LQR(cfg.eqn_config)
+        cfg = lqr_d20(a.iters, a.log_freq, dtype, a.batch, a.valid, a.config)
+        bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
         sp = psol.ActorCriticSolver(cfg, bsde, seed=a.seed, sampler="host")
         if init is None:  # every run starts from the first run's weights, in float64
             init = {"critic": sp.model_critic.NN_value.export_params(),
@@ -110,7 +123,7 @@ def main():
         from oracle import equations as oeq
         from oracle import solver as osol
         torch.set_num_threads(min(16, os.cpu_count() or 1))
-        cfg = lqr_d20(a.iters, a.log_freq, "float64", a.batch, a.valid)
+        cfg = lqr_d20(a.iters, a.log_freq, "float64", a.batch, a.valid, a.config)
         so = osol.ActorCriticSolver(cfg, oeq.make(cfg.eqn_config), params=init)
         np.random.seed(a.data_seed)
         t0 = time.perf_counter()
@@ -123,6 +136,7 @@ def main():
     if a.oracle_from:
         prev = json.load(open(a.oracle_from))
         assert (prev["iters"], prev["log_freq"], prev["batch"], prev["valid"]) == (a.iters, a.log_freq, a.batch, a.valid)
+        assert prev["config"].split()[0] == a.config
         res["runs"]["oracle"] = dict(prev["runs"]["oracle"], source=a.oracle_from)
     if "oracle" in res["runs"]:
         ref = np.array(res["runs"]["oracle"]["history"]["err_value"])
