@@ -185,3 +185,55 @@ def test_fused_bptt_kernel_matches_step_loop(name, d, hidden, scheme):
         ops.BPTT_MODE = "fused"
     for a, b in zip(grads["fused"], grads["loop"]):
         assert rel_close(a.cpu(), b.cpu(), 1e-10)
+
+
+@pytest.mark.parametrize("name,d,hidden,B", [("LQR", 20, (256, 256, 256, 256), 20), ("EKN", 10, (256, 7), 1),
+                                             ("VDP", 20, (4, 256), 16)])
+def test_fused_nn_limits_fwd_and_bptt(name, d, hidden, B):
+    """Widths at DPAC_MLP_MAX_WIDTH, 4 hidden layers, tiny and odd widths, B = 1: the
+    fused forward against the oracle and the fused BPTT against the reference loop."""
+    N, T = 8, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme="adaptive")
+    eo = oeq.make(cfg.eqn_config)
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, onet = actor_pair(cfg, torch.float64)
+    np.random.seed(31)
+    x0 = np.random.uniform(-0.3, 0.3, size=(B, d))
+    dw = np.random.standard_normal((B, d, N))
+    xr, dtr, cr = eo.propagate_adaptive(B, x0, dw, onet, False, T, N, False)
+    x0t = torch.as_tensor(x0, device=DEV)
+    dwt = torch.as_tensor(dw, device=DEV).permute(2, 0, 1).contiguous()
+    x, dt, coef, _, _, _, _ = ops.rollout_nn(ep.params(), _lib.SCHEME_ADAPTIVE, x0t, dwt, T, N, net.mlp_view())
+    np.testing.assert_array_equal(coef.cpu().numpy(), cr.numpy())
+    assert rel_close(x.permute(1, 2, 0).cpu(), xr, 1e-10)
+    grads = {}
+    try:
+        for mode in ("loop", "fused"):
+            ops.BPTT_MODE = mode
+            y, disc, xN = ops.actor_rollout_nn(ep.params(), _lib.SCHEME_ADAPTIVE, x0t, dwt, T, N, net)
+            grads[mode] = torch.autograd.grad(torch.mean(y + disc * torch.sum(xN, 1)), net.trainable_variables())
+    finally:
+        ops.BPTT_MODE = "fused"
+    for a, b in zip(grads["fused"], grads["loop"]):
+        assert rel_close(a.cpu(), b.cpu(), 1e-10)
+
+
+def test_fused_bptt_fp32_ekn():
+    """float32 fused BPTT through the Eikonal head vs the float32 reference loop."""
+    B, N, T = 64, 20, 0.2
+    cfg = full_config("EKN", 20, N=N, hidden=(200, 200, 200), scheme="adaptive", dtype="float32")
+    ep = peq.EKN(cfg.eqn_config)
+    net, _ = actor_pair(cfg, torch.float32)
+    eqp = ep.params()
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=4, dtype=torch.float32, device=DEV)
+    grads = {}
+    try:
+        for mode in ("loop", "fused"):
+            ops.BPTT_MODE = mode
+            y, disc, xN = ops.actor_rollout_nn(eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, net)
+            grads[mode] = torch.autograd.grad(torch.mean(y + disc * torch.sum(xN * xN, 1)),
+                                              net.trainable_variables())
+    finally:
+        ops.BPTT_MODE = "fused"
+    for a, b in zip(grads["fused"], grads["loop"]):
+        assert rel_close(a.cpu(), b.cpu(), 1e-4)
