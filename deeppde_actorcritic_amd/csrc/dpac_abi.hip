@@ -20,6 +20,10 @@ bool has_dim_lqr(int);
 bool has_dim_vdp(int);
 bool has_dim_ekn(int);
 bool has_dim_lqrvar(int);
+int64_t mlp_param_grads_ws_bytes(int dtype, int64_t rows, const dpac_mlp& net);
+int mlp_param_grads_launch(int dtype, int64_t rows, const dpac_mlp& net, double gamma_scale,
+                           const void* x, int64_t ldx, const void* z, const void* G, void* ws,
+                           void* out, hipStream_t s);
 
 namespace {
 thread_local std::string g_err;
@@ -119,6 +123,23 @@ int check_mlp(const dpac_eqn_params* eq, const dpac_mlp* actor) {
     return fail(DPAC_EINVAL, "actor: output width %d must be control_dim%s (%d)",
                 actor->width[L + 1], actor->ekn_head ? " + 1" : "",
                 eq->control_dim + actor->ekn_head);
+  return DPAC_OK;
+}
+
+// A dpac_mlp for the row-parallel kernels (no equation attached).
+int check_net(const dpac_mlp* net) {
+  if (!net) return fail(DPAC_EINVAL, "MLP pointer is NULL");
+  const int L = net->n_hidden;
+  if (L < 1 || L > DPAC_MLP_MAX_HIDDEN)
+    return fail(DPAC_EINVAL, "n_hidden must be in [1, %d] (got %d)", DPAC_MLP_MAX_HIDDEN, L);
+  for (int i = 0; i <= L + 1; ++i) {
+    if (net->width[i] < 1 || net->width[i] > DPAC_MLP_MAX_WIDTH)
+      return fail(DPAC_EINVAL, "width[%d] = %d outside [1, %d]", i, net->width[i],
+                  DPAC_MLP_MAX_WIDTH);
+    if (!net->bn_scale[i] || !net->bn_shift[i])
+      return fail(DPAC_EINVAL, "bn_scale/bn_shift[%d] is NULL", i);
+  }
+  if (!net->bias) return fail(DPAC_EINVAL, "bias is NULL");
   return DPAC_OK;
 }
 
@@ -387,6 +408,37 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
   a.g_x_out = g_xN; a.g_disc_out = g_disc; a.g_y_out = g_y; a.g_G = G; a.g_x = g_x0;
   a.stream = (hipStream_t)stream;
   return launch(a);
+}
+
+int64_t dpac_mlp_param_grads_workspace(int32_t dtype, int64_t rows, const dpac_mlp* net) {
+  if (check_net(net)) return -1;
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype), -1;
+  if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1"), -1;
+  ok();
+  return mlp_param_grads_ws_bytes(dtype, rows, *net);
+}
+
+int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, double gamma_scale,
+                         const void* x, int64_t ldx, const void* save_z, const void* G,
+                         void* workspace, int64_t workspace_bytes, void* grads, void* stream) {
+  if (int e = check_net(net)) return e;
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
+  if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1 (got %lld)", (long long)rows);
+  if (ldx < net->width[0]) return fail(DPAC_EINVAL, "ldx (%lld) < width[0] (%d)", (long long)ldx,
+                                       net->width[0]);
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(save_z);
+  DPAC_REQUIRE(G);
+  DPAC_REQUIRE(workspace);
+  DPAC_REQUIRE(grads);
+  const int64_t need = mlp_param_grads_ws_bytes(dtype, rows, *net);
+  if (workspace_bytes < need)
+    return fail(DPAC_EINVAL, "workspace too small: %lld bytes, need %lld",
+                (long long)workspace_bytes, (long long)need);
+  const int r = mlp_param_grads_launch(dtype, rows, *net, gamma_scale, x, ldx, save_z, G,
+                                       workspace, grads, (hipStream_t)stream);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
 }
 
 int dpac_flag_init(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype, int64_t num_sample,

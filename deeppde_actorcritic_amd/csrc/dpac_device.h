@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "dpac.h"
+#include "dpac_mfma.h"
 
 namespace dpac {
 

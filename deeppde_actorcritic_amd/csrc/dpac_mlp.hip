@@ -1,0 +1,116 @@
+// dpac_mlp.hip — host side of the equation-independent MLP kernels (parameter
+// gradients over independent rows, dpac_mlp_grad.h), compiled once for both
+// dtypes.  Argument checking and error strings live in dpac_abi.hip.
+#include <algorithm>
+
+#include "dpac_mlp_grad.h"
+
+namespace dpac {
+
+namespace {
+
+template <typename T>
+PgArgs<T> pg_args(const dpac_mlp& net, int64_t rows, const void* x, int64_t ldx, const void* z,
+                  const void* G) {
+  PgArgs<T> a{};
+  const int L = net.n_hidden;
+  a.rows = rows;
+  a.L = L;
+  int zt = 0, gt = 0, sw = 0;
+  for (int i = 0; i <= L + 1; ++i) {
+    a.width[i] = net.width[i];
+    a.scale[i] = (const T*)net.bn_scale[i];
+    a.shift[i] = (const T*)net.bn_shift[i];
+    a.zoff[i] = i == 0 ? 0 : zt;
+    if (i > 0) zt += net.width[i];
+    a.goff[i] = gt;
+    gt += net.width[i];
+    sw += net.width[i];
+  }
+  a.bias = (const T*)net.bias;
+  a.x = (const T*)x;
+  a.z = (const T*)z;
+  a.G = (const T*)G;
+  a.ldx = (int)ldx;
+  a.ztot = zt;
+  a.gtot = gt;
+  int64_t o = 0;
+  for (int i = 0; i <= L + 1; ++i) { a.off_gamma[i] = o; o += net.width[i]; }
+  for (int i = 0; i <= L + 1; ++i) { a.off_beta[i] = o; o += net.width[i]; }
+  for (int i = 0; i <= L; ++i) { a.off_W[i] = o; o += (int64_t)net.width[i] * net.width[i + 1]; }
+  a.ptot = o;
+  (void)sw;
+  return a;
+}
+
+template <typename T>
+int64_t pg_chunk_rows(int64_t rows, int64_t max_ld) {
+  // ~192 chunks: 4-8 workgroups per CU over the (group, layer) grid, and a
+  // partial buffer the reduce reads in ~10 us.  A chunk's rows are addressed
+  // through 32-bit buffer descriptors: keep them below 2 GiB.
+  constexpr int SR = PgCfg<T>::SR;
+  int64_t per = (rows + 191) / 192;
+  const int64_t cap = (((int64_t)1 << 31) - 1) / (max_ld * (int64_t)sizeof(T)) / SR * SR;
+  per = (per + SR - 1) / SR * SR;
+  return std::max<int64_t>(std::min(per, cap), SR);
+}
+
+template <typename T>
+int64_t max_ld(const PgArgs<T>& a) {
+  return std::max<int64_t>(std::max(a.ldx, a.ztot), a.gtot);
+}
+
+template <typename T>
+int64_t ws_bytes(int64_t rows, const dpac_mlp& net) {
+  const PgArgs<T> a = pg_args<T>(net, rows, nullptr, net.width[0], nullptr, nullptr);
+  const int64_t per = pg_chunk_rows<T>(rows, max_ld(a));
+  const int64_t nch = (rows + per - 1) / per;
+  return nch * a.ptot * (int64_t)sizeof(T);
+}
+
+template <typename T>
+int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x, int64_t ldx,
+           const void* z, const void* G, void* ws, void* out, hipStream_t s) {
+  PgArgs<T> a = pg_args<T>(net, rows, x, ldx, z, G);
+  a.rows_per_chunk = pg_chunk_rows<T>(rows, max_ld(a));
+  a.part = (T*)ws;
+  const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
+  int maxw = 0;
+  for (int i = 1; i <= a.L + 1; ++i) maxw = std::max(maxw, a.width[i]);
+  constexpr int CW = 64 * PgCfg<T>::NTJ;
+  // one launch per layer: the row-tile count of dW_l (ceil(width[l]/16)) is a
+  // template bin, 1 / 2 / 4 / 8 / 13 / 16
+  for (int l = 0; l <= a.L; ++l) {
+    const int nti = (a.width[l] + 15) / 16;
+    const dim3 grid((unsigned)nch, (unsigned)((a.width[l + 1] + CW - 1) / CW));
+#define DPAC_PG(NT) hipLaunchKernelGGL((k_param_grads<T, NT>), grid, dim3(kPgThreads), 0, s, a, l)
+    if (nti <= 1) DPAC_PG(1);
+    else if (nti <= 2) DPAC_PG(2);
+    else if (nti <= 4) DPAC_PG(4);
+    else if (nti <= 8) DPAC_PG(8);
+    else if (nti <= 13) DPAC_PG(13);
+    else DPAC_PG(16);
+#undef DPAC_PG
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
+  (void)maxw;
+  const int64_t n = a.ptot + a.width[a.L + 1];
+  hipLaunchKernelGGL(k_param_grads_reduce<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     a, (int)nch, (T)gamma_scale, (T*)out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+int64_t mlp_param_grads_ws_bytes(int dtype, int64_t rows, const dpac_mlp& net) {
+  return dtype == DPAC_F64 ? ws_bytes<double>(rows, net) : ws_bytes<float>(rows, net);
+}
+
+int mlp_param_grads_launch(int dtype, int64_t rows, const dpac_mlp& net, double gamma_scale,
+                           const void* x, int64_t ldx, const void* z, const void* G, void* ws,
+                           void* out, hipStream_t s) {
+  return dtype == DPAC_F64 ? launch<double>(rows, net, gamma_scale, x, ldx, z, G, ws, out, s)
+                           : launch<float>(rows, net, gamma_scale, x, ldx, z, G, ws, out, s);
+}
+
+}  // namespace dpac

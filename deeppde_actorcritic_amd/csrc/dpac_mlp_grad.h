@@ -1,0 +1,276 @@
+// dpac_mlp_grad.h — parameter gradients of a DeepNN (solver.py:227-278) from the
+// backward chain's G and the forward's saved pre-BN outputs, over R independent
+// rows (the actor's N*B BPTT rows or the critic G network's N*B rows).
+//
+// With s_i = gamma_i/sqrt(1+eps), a_0 = BN_0(x), a_i = y_i + relu(y_i),
+// y_i = beta_i + z_i*s_i (i = 1..L) and G_i = dL/d(output of BN_i):
+//   dW_i     = Σ_r a_i[r]^T (G_{i+1}[r] ⊙ s_{i+1})          [w_i x w_{i+1}]
+//   dbeta_i  = Σ_r G_i[r]
+//   dgamma_i = rs · Σ_r G_i[r] ⊙ zin_i[r],  zin_0 = x, zin_i = z_i, zin_{L+1} = z_{L+1} + b
+//   db       = s_{L+1} ⊙ dbeta_{L+1}
+// (what the reference's GradientTape produces for the trainable variables of
+// DeepNN, solver.py:88,95).
+//
+// k_param_grads: workgroup (chunk c, column group g, layer i) = 4 wavefronts.
+// Rows of the chunk are staged SR at a time through LDS — a_i (BN + activation
+// applied while loading z_i) as the MFMA A operand (transposed: the reduction
+// runs over rows) and G_{i+1} ⊙ s_{i+1} for the group's CW columns as B — and
+// every wavefront accumulates its 16 x NTJ output tiles of dW_i in registers
+// across the whole chunk.  The BN column sums ride on the same loads.  Each
+// workgroup writes its chunk's partial; k_param_grads_reduce sums the chunks in
+// a fixed order (deterministic, no atomics) and applies rs and s_{L+1}.
+#pragma once
+
+#include "dpac_device.h"
+
+namespace dpac {
+
+constexpr int kPgThreads = 256;
+constexpr int kPgMaxTiles = DPAC_MLP_MAX_WIDTH / 16;
+constexpr int kPgQ = DPAC_MLP_MAX_WIDTH / 64;  // A-stage columns per thread
+
+template <typename T>
+struct PgCfg;
+template <>
+struct PgCfg<float> {
+  static constexpr int NTJ = 2, SR = 16;  // 128 accumulator registers (AGPRs)
+};
+template <>
+struct PgCfg<double> {
+  static constexpr int NTJ = 1, SR = 16;
+};
+
+template <typename T>
+struct PgArgs {
+  int64_t rows, rows_per_chunk;
+  int L;
+  int width[DPAC_MLP_MAX_HIDDEN + 2];
+  const T* scale[DPAC_MLP_MAX_HIDDEN + 2];
+  const T* shift[DPAC_MLP_MAX_HIDDEN + 2];
+  const T* bias;
+  const T *x, *z, *G;
+  int ldx, ztot, gtot;
+  int zoff[DPAC_MLP_MAX_HIDDEN + 2];  // column of z_i in a z row (i >= 1)
+  int goff[DPAC_MLP_MAX_HIDDEN + 2];  // column of G_i in a G row
+  int64_t ptot;                       // elements per chunk partial (= flat size without b)
+  int64_t off_gamma[DPAC_MLP_MAX_HIDDEN + 2], off_beta[DPAC_MLP_MAX_HIDDEN + 2];
+  int64_t off_W[DPAC_MLP_MAX_HIDDEN + 1];
+  T* part;  // [nchunks][ptot]
+};
+
+template <typename T>
+__device__ __forceinline__ T buf_load_elem(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  uint32_t w[sizeof(T) / 4];
+  buf_load_dwords<sizeof(T) / 4>(r, voff, w);
+  T v;
+  __builtin_memcpy(&v, &w[0], sizeof(T));
+  return v;
+}
+
+// One sub-chunk's global loads, issued before the MFMA phase of the previous one.
+template <typename T, int SR, int NTJ>
+struct PgStage {
+  T a[SR / 4][kPgQ];   // zin_l (A source) at rows wave + 4m, columns lane + 64q
+  T g0[SR / 4];        // layer 0 only: G_0 at column lane (BN_0 sums)
+  T gb[SR / 4][NTJ];   // G_{l+1} at columns col0 + lane + 64q
+  T zb[SR / 4][NTJ];   // zin_{l+1} (pre-bias) at the same places
+};
+
+// Workgroup (chunk c, column group g, layer l): the chunk's partial of dW_l for
+// B columns [g*CW, (g+1)*CW), plus the BN_{l+1} column sums of those columns
+// (and, layer 0 / group 0, the BN_0 sums).
+template <typename T, int NTI>
+__global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, const int l) {
+  using MF = Mfma<T>;
+  constexpr int NTJ = PgCfg<T>::NTJ, SR = PgCfg<T>::SR;
+  constexpr int CW = 64 * NTJ;                     // B columns per workgroup
+  constexpr int LDA = DPAC_MLP_MAX_WIDTH + 16;     // row strides: lanes of a k-quad
+  constexpr int LDB = CW + 16;                     // land 16 words apart
+  constexpr uint32_t ES = sizeof(T);
+  __shared__ T sA[SR * LDA];
+  __shared__ T sB[SR * LDB];
+  const int grp = blockIdx.y;
+  const int K = a.width[l], H = a.width[l + 1];
+  const int col0 = grp * CW;
+  if (col0 >= H) return;  // whole workgroup: no barrier reached yet
+  // NTI >= ceil(K/16) row tiles (a compile-time count: the MFMA loop is
+  // straight-line code); tiles past K multiply zero padding
+  const int tid = threadIdx.x, lane = tid % 64;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / 64);
+  const int64_t chunk = blockIdx.x;
+  const int64_t r_begin = chunk * a.rows_per_chunk;
+  const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
+  const bool first = l == 0 && grp == 0;  // also sums BN_0
+  const bool last = l == a.L;             // zin_{L+1} = z_{L+1} + bias
+  const T* srcA = l == 0 ? a.x : a.z + a.zoff[l];
+  const int64_t ldA = l == 0 ? a.ldx : a.ztot;
+  const T* gA = a.G + a.goff[0];
+  const T* gB = a.G + a.goff[l + 1] + col0;
+  const T* zB = a.z + a.zoff[l + 1] + col0;
+  constexpr int kpad = 16 * NTI;
+
+  // per-thread constants: A columns lane + 64q, B columns col0 + lane + 64q
+  T sa[kPgQ], ha[kPgQ], sbv[NTJ], bbv[NTJ];
+  uint32_t offA[kPgQ], offB[NTJ];
+#pragma unroll
+  for (int q = 0; q < kPgQ; ++q) {
+    const int k = lane + 64 * q;
+    sa[q] = k < K ? a.scale[l][k] : T(0);
+    ha[q] = k < K ? a.shift[l][k] : T(0);
+    offA[q] = k < K ? (uint32_t)k * ES : kOOB;
+  }
+#pragma unroll
+  for (int q = 0; q < NTJ; ++q) {
+    const int h = col0 + lane + 64 * q;
+    sbv[q] = h < H ? a.scale[l + 1][h] : T(0);
+    bbv[q] = (h < H && last) ? a.bias[h] : T(0);
+    offB[q] = h < H ? (uint32_t)(lane + 64 * q) * ES : kOOB;
+  }
+  const uint32_t offG0 = (first && lane < K) ? (uint32_t)lane * ES : kOOB;
+  T cs0_b = 0, cs0_s = 0, csb_b[NTJ], csb_s[NTJ];
+#pragma unroll
+  for (int q = 0; q < NTJ; ++q) csb_b[q] = csb_s[q] = T(0);
+  typename MF::acc_t acc[NTI][NTJ];
+#pragma unroll
+  for (int ti = 0; ti < NTI; ++ti)
+#pragma unroll
+    for (int jj = 0; jj < NTJ; ++jj) acc[ti][jj] = typename MF::acc_t{0, 0, 0, 0};
+
+  // Loads of the SR rows starting at r0: descriptors based at row r0 whose range
+  // ends at the chunk's last row, so rows past it read 0; masked columns carry
+  // kOOB offsets (kOOB + a row offset < 2^32 stays out of range).  Every load is
+  // unconditional: a select on a load result would force its wait right there.
+  auto issue = [&](int64_t r0, PgStage<T, SR, NTJ>& st) {
+    const int64_t nr = r_end - r0;  // >= 1
+    const auto rA = make_rsrc(srcA + r0 * ldA, (uint32_t)(((nr - 1) * ldA + K) * ES));
+    const auto rG = make_rsrc(gA + r0 * a.gtot, (uint32_t)(((nr - 1) * a.gtot + K) * ES));
+    const auto rB = make_rsrc(gB + r0 * a.gtot, (uint32_t)(((nr - 1) * a.gtot + (H - col0)) * ES));
+    const auto rZ = make_rsrc(zB + r0 * a.ztot, (uint32_t)(((nr - 1) * a.ztot + (H - col0)) * ES));
+#pragma unroll
+    for (int m = 0; m < SR / 4; ++m) {
+      const uint32_t rl = (uint32_t)(wave + 4 * m);
+#pragma unroll
+      for (int q = 0; q < kPgQ; ++q) st.a[m][q] = buf_load_elem<T>(rA, offA[q] + rl * (uint32_t)ldA * ES);
+      st.g0[m] = buf_load_elem<T>(rG, offG0 + rl * (uint32_t)a.gtot * ES);
+#pragma unroll
+      for (int q = 0; q < NTJ; ++q) {
+        st.gb[m][q] = buf_load_elem<T>(rB, offB[q] + rl * (uint32_t)a.gtot * ES);
+        st.zb[m][q] = buf_load_elem<T>(rZ, offB[q] + rl * (uint32_t)a.ztot * ES);
+      }
+    }
+  };
+
+  PgStage<T, SR, NTJ> st;
+  issue(r_begin, st);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += SR) {
+    __syncthreads();  // the previous sub-chunk's MFMA reads are done
+#pragma unroll
+    for (int m = 0; m < SR / 4; ++m) {
+      const int rl = wave + 4 * m;
+#pragma unroll
+      for (int q = 0; q < kPgQ; ++q) {
+        const int k = lane + 64 * q;
+        if (64 * q >= kpad) continue;  // compile-time
+        const T zi = st.a[m][q];
+        const T y = ha[q] + zi * sa[q];  // the forward's expression (FwdEpi / write_a0)
+        const T v = l == 0 ? y : y + fmax(y, T(0));
+        if (k < kpad) sA[rl * LDA + k] = k < K ? v : T(0);  // rows past the end: z = 0 gives
+      }                                                      // a = shift, masked by G = 0
+      cs0_b += st.g0[m];  // G_0 reads 0 unless layer 0 / group 0
+      cs0_s += st.g0[m] * st.a[m][0];
+#pragma unroll
+      for (int q = 0; q < NTJ; ++q) {
+        const T gv = st.gb[m][q];
+        sB[rl * LDB + lane + 64 * q] = gv * sbv[q];
+        csb_b[q] += gv;
+        csb_s[q] += gv * (st.zb[m][q] + bbv[q]);  // bbv = 0 unless the output layer
+      }
+    }
+    __syncthreads();
+    if (r0 + SR < r_end) issue(r0 + SR, st);  // in flight during the MFMA phase
+    const int kk = lane >> 4, ii = lane & 15;
+    // Branch-free: B column tiles past H hold zeros (their products are dropped
+    // at the store), so every wave runs the same NTI x NTJ MFMAs per k-step.
+#pragma unroll
+    for (int ks = 0; ks < SR / 4; ++ks) {
+      T bf[NTJ], af[NTI];
+#pragma unroll
+      for (int jj = 0; jj < NTJ; ++jj) bf[jj] = sB[(4 * ks + kk) * LDB + (wave + 4 * jj) * 16 + ii];
+#pragma unroll
+      for (int ti = 0; ti < NTI; ++ti) af[ti] = sA[(4 * ks + kk) * LDA + ti * 16 + ii];
+#pragma unroll
+      for (int ti = 0; ti < NTI; ++ti)
+#pragma unroll
+        for (int jj = 0; jj < NTJ; ++jj) acc[ti][jj] = MF::mma(af[ti], bf[jj], acc[ti][jj]);
+    }
+  }
+
+  // ---- this chunk's partial dW_l ----
+  T* part = a.part + chunk * a.ptot;
+#pragma unroll
+  for (int ti = 0; ti < NTI; ++ti) {
+#pragma unroll
+    for (int jj = 0; jj < NTJ; ++jj) {
+      const int h = col0 + (wave + 4 * jj) * 16 + (lane & 15);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int k = ti * 16 + MF::row(lane, v);
+        if (k < K && h < H) part[a.off_W[l] + (int64_t)k * H + h] = acc[ti][jj][v];
+      }
+    }
+  }
+  // ---- BN column sums: combine the 4 wavefronts (row phases) through LDS ----
+  __syncthreads();  // LDS reuse
+  T* red = sA;  // [4 waves][2][CW] (B side), then [4 waves][2][64] (BN_0)
+#pragma unroll
+  for (int q = 0; q < NTJ; ++q) {
+    red[(wave * 2 + 0) * CW + lane + 64 * q] = csb_b[q];
+    red[(wave * 2 + 1) * CW + lane + 64 * q] = csb_s[q];
+  }
+  T* red0 = sA + 8 * CW;
+  red0[(wave * 2 + 0) * 64 + lane] = cs0_b;
+  red0[(wave * 2 + 1) * 64 + lane] = cs0_s;
+  __syncthreads();
+  if (tid < CW && col0 + tid < H) {
+    T sb = 0, ss = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sb += red[(w * 2 + 0) * CW + tid];
+      ss += red[(w * 2 + 1) * CW + tid];
+    }
+    part[a.off_beta[l + 1] + col0 + tid] = sb;
+    part[a.off_gamma[l + 1] + col0 + tid] = ss;
+  }
+  if (first && tid < K) {
+    T sb = 0, ss = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sb += red0[(w * 2 + 0) * 64 + tid];
+      ss += red0[(w * 2 + 1) * 64 + tid];
+    }
+    part[a.off_beta[0] + tid] = sb;
+    part[a.off_gamma[0] + tid] = ss;
+  }
+}
+
+// out[p] = Σ_c part[c][p] in chunk order; gamma entries times rs; the bias
+// gradient db = s_{L+1} ⊙ dbeta_{L+1} appended at out[ptot ...].
+template <typename T>
+__global__ __launch_bounds__(256) void k_param_grads_reduce(const PgArgs<T> a, int nchunks,
+                                                            T gamma_scale, T* out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int L = a.L, Hout = a.width[L + 1];
+  if (p >= a.ptot + Hout) return;
+  const bool is_b = p >= a.ptot;
+  const int64_t src = is_b ? a.off_beta[L + 1] + (p - a.ptot) : p;
+  T s = 0;
+  for (int c = 0; c < nchunks; ++c) s += a.part[(int64_t)c * a.ptot + src];
+  if (is_b) {
+    s = a.scale[L + 1][p - a.ptot] * s;
+  } else if (p < a.off_beta[0]) {  // gamma block comes first
+    s = gamma_scale * s;
+  }
+  out[p] = s;
+}
+
+}  // namespace dpac

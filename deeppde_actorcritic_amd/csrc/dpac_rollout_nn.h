@@ -31,27 +31,6 @@ constexpr int kNnPrefetch = 8;  // k-steps of B in flight per tile
 // The ring reads A up to k < 4 * roundup(ceil(K/4), kNnPrefetch) <= 256 for K <= 256.
 static_assert(DPAC_MLP_MAX_WIDTH <= 256 && kNnLd >= 256, "A reads stay inside an LDS row");
 
-// 16x16x4 MFMA for one precision.  A[row l&15][k l>>4], B[k l>>4][col l&15];
-// the accumulator's element i of lane l is C[row(l, i)][l&15].
-template <typename T>
-struct Mfma;
-template <>
-struct Mfma<float> {
-  using acc_t = __attribute__((ext_vector_type(4))) float;
-  __device__ static acc_t mma(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  __device__ static int row(int lane, int i) { return (lane >> 4) * 4 + i; }
-};
-template <>
-struct Mfma<double> {
-  using acc_t = __attribute__((ext_vector_type(4))) double;
-  __device__ static acc_t mma(double a, double b, acc_t c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-  }
-  __device__ static int row(int lane, int i) { return (lane >> 4) + 4 * i; }  // f64 C map
-};
-
 // The MLP as the kernel sees it (from dpac_mlp, include/dpac.h).
 template <typename T>
 struct NnMlp {

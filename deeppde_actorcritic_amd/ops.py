@@ -215,7 +215,11 @@ class _ActorRolloutNN(torch.autograd.Function):
         else:
             G = _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b,
                            widths, gx_in, gd_in, gy_in)
-        # parameter gradients over all N*B rows
+        if PARAM_GRADS == "kernel":
+            grads = mlp_param_grads(MlpView(s, bet, Ws, b, ekn), x[:N].reshape(N * B, d),
+                                    z.reshape(N * B, -1), G_all(G).reshape(N * B, -1), params)
+            return (None,) * 8 + tuple(grads)
+        # parameter gradients over all N*B rows (PyTorch reference path)
         rows = lambda tt: tt.reshape(N * B, -1)
         zin = [x[:N]] + [zl[i] for i in range(1, L + 1)] + [zl[L + 1] + b]
         dgam = [rs * torch.sum(rows(G[i] * zin[i]), 0) for i in range(L + 2)]
@@ -234,6 +238,62 @@ class _ActorRolloutNN(torch.autograd.Function):
 # "fused": the reverse time loop as one dpac_rollout_nn_bwd launch; "loop": the
 # reference implementation of the same loop, dpac_step_bwd + PyTorch per step.
 BPTT_MODE = "fused"
+# "kernel": parameter gradients from dpac_mlp_param_grads (one launch + reduce);
+# "torch": the same sums as PyTorch products/reductions (test reference).
+PARAM_GRADS = "kernel"
+
+
+def G_all(G):
+    """The [N, B, Σ widths] buffer behind the per-layer views of _bptt_fused / _bptt_loop."""
+    base = G[0]._base if G[0]._base is not None else None
+    if base is not None and all(g._base is base for g in G) and base.is_contiguous():
+        return base
+    return torch.cat(G, dim=-1).contiguous()
+
+
+_WS_CACHE = {}
+
+
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    """A reusable device scratch buffer (one per device, grown on demand; the
+    stream order of its users makes sharing safe)."""
+    key = (device.type, device.index)
+    ws = _WS_CACHE.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = _WS_CACHE[key] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+    return ws
+
+
+def bn_rs_host(dtype) -> float:
+    """1/sqrt(1 + 1e-6) rounded as DeepNN.bn_rs is (solver.py BN_EPS), on the host: the
+    device copy must not be read inside a captured graph."""
+    return float(torch.rsqrt(torch.tensor(1.0 + 1e-6, dtype=dtype)))
+
+
+def mlp_param_grads(view: "MlpView", x, z, G, like):
+    """Gradients of DeepNN's trainable variables (order of trainable_variables()) from
+    the backward chain's G [R, Σ widths], the saved z [R, Σ widths[1:]] and the
+    network input x [R, d]; one dpac_mlp_param_grads launch.  `like` gives the
+    parameter shapes."""
+    _require_gpu(x, z, G)
+    R = x.shape[0]
+    dt = _dtype_id(x)
+    nbytes = _lib.load().dpac_mlp_param_grads_workspace(dt, R, ctypes.byref(view.struct))
+    if nbytes < 0:
+        raise _lib.DpacError("dpac_mlp_param_grads_workspace", nbytes, _lib.load().dpac_last_error().decode())
+    ws = _workspace(int(nbytes), x.device)
+    total = sum(p.numel() for p in like)
+    flat = torch.empty(total, dtype=x.dtype, device=x.device)
+    if x.stride(1) != 1 or not z.is_contiguous() or not G.is_contiguous():
+        raise ValueError("mlp_param_grads: x needs unit column stride, z and G contiguous")
+    call("dpac_mlp_param_grads", dt, R, ctypes.byref(view.struct), bn_rs_host(x.dtype),
+         ctypes.c_void_p(x.data_ptr()),
+         x.stride(0), _ptr(z), _ptr(G), _ptr(ws), ws.numel(), _ptr(flat), _stream(x))
+    out, o = [], 0
+    for p in like:
+        out.append(flat[o:o + p.numel()].view(p.shape))
+        o += p.numel()
+    return out
 
 
 def _bptt_fused(eqp, scheme, T, N, ekn, L, x, u, dw, z, flag, disc_t, s, bet, Ws, b, widths,

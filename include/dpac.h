@@ -271,6 +271,28 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
                         const int32_t* save_flag, const void* save_disc, const void* g_xN,
                         const void* g_disc, const void* g_y, void* G, void* g_x0, void* stream);
 
+/* ---- parameter gradients of a dpac_mlp over independent rows -------------
+ * What GradientTape returns for DeepNN's trainable variables (solver.py:88,95
+ * through solver.py:260-271), given the backward chain's G [rows][Σ_i width[i]]
+ * (as written by dpac_rollout_nn_bwd or dpac_mlp_rows_bwd) and the forward's
+ * save_z [rows][Σ_{i>=1} width[i]]; x [rows] with row stride ldx is the network
+ * input.  With s_i = bn_scale[i], a_0 = bn_shift[0] + x*s_0 and
+ * a_i = y_i + relu(y_i), y_i = bn_shift[i] + z_i*s_i:
+ *   dW_i = Σ_r a_i^T (G_{i+1} ⊙ s_{i+1}),  dbeta_i = Σ_r G_i,
+ *   dgamma_i = gamma_scale · Σ_r G_i ⊙ zin_i  (zin_0 = x, zin_{L+1} = z_{L+1} + bias),
+ *   dbias = s_{L+1} ⊙ dbeta_{L+1};
+ * gamma_scale = 1/sqrt(1 + 1e-6) (d bn_scale / d gamma).  grads is one flat
+ * buffer in DeepNN's variable order: gamma_0..gamma_{L+1}, beta_0..beta_{L+1},
+ * W_0..W_L (row-major), bias.  The sums over rows run chunk-wise into
+ * `workspace` (size from dpac_mlp_param_grads_workspace, -1 on a bad argument)
+ * and are combined in a fixed order: deterministic.  weight[] of `net` is not
+ * read (may be NULL).  The reference has no such entry point: this replaces the
+ * TF-internal gradient ops of the Dense / BatchNormalization layers. */
+int64_t dpac_mlp_param_grads_workspace(int32_t dtype, int64_t rows, const dpac_mlp* net);
+int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, double gamma_scale,
+                         const void* x, int64_t ldx, const void* save_z, const void* G,
+                         void* workspace, int64_t workspace_bytes, void* grads, void* stream);
+
 /* ---- device equation coefficients (for parity tests and metrics) -------
  * Evaluates one Equation method row-wise on x [B][d] (and u [B][c] where the
  * method takes a control): drift/sigma/w/Z/V_true/u_true/V_grad_true/b_tf

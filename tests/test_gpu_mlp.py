@@ -1,0 +1,134 @@
+"""dpac_mlp_param_grads (DeepNN parameter gradients over independent rows, the
+Dense/BatchNormalization gradient ops of solver.py:227-278 under the tape of
+solver.py:88,95) against a plain PyTorch float64 statement of the same sums, and
+inside the actor's BPTT against the PyTorch product path.
+
+Tolerances: float64 |a-b| <= 1e-11 (1+|b|) (only the summation order differs);
+float32 vs the float64 reference: 2e-5 (1+|b|) relative to the largest entry.
+"""
+import pytest
+import torch
+
+from deeppde_actorcritic_amd import _lib, ops
+from deeppde_actorcritic_amd import equation as peq
+from deeppde_actorcritic_amd.config import set_floatx
+from deeppde_actorcritic_amd import solver as psol
+from tests.helpers import full_config, rel_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def random_net(widths, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    L = len(widths) - 2
+    mk = lambda *s: (torch.rand(*s, generator=g, dtype=torch.float64) - 0.5).to(dtype).to(DEV)
+    scales = [mk(w) + 0.7 for w in widths]
+    shifts = [mk(w) for w in widths]
+    Ws = [mk(widths[i], widths[i + 1]) for i in range(L + 1)]
+    b = mk(widths[-1])
+    return scales, shifts, Ws, b
+
+
+def reference_grads(widths, scales, shifts, Ws, b, rs, x, z, G):
+    """The sums of include/dpac.h dpac_mlp_param_grads, in float64 PyTorch."""
+    f = lambda t: t.double()
+    L = len(widths) - 2
+    zo = [0]
+    for w in widths[1:]:
+        zo.append(zo[-1] + w)
+    go = [0]
+    for w in widths:
+        go.append(go[-1] + w)
+    zl = [None] + [f(z[:, zo[i - 1]:zo[i]]) for i in range(1, L + 2)]
+    Gl = [f(G[:, go[i]:go[i + 1]]) for i in range(L + 2)]
+    s = [f(t) for t in scales]
+    sh = [f(t) for t in shifts]
+    zin = [f(x)] + zl[1:L + 1] + [zl[L + 1] + f(b)]
+    dgam = [rs * torch.sum(Gl[i] * zin[i], 0) for i in range(L + 2)]
+    dbet = [torch.sum(Gl[i], 0) for i in range(L + 2)]
+    A = [sh[0] + f(x) * s[0]]
+    for i in range(1, L + 1):
+        y = sh[i] + zl[i] * s[i]
+        A.append(y + torch.relu(y))
+    dW = [A[i].t() @ (Gl[i + 1] * s[i + 1]) for i in range(L + 1)]
+    db = torch.sum(Gl[L + 1] * s[L + 1], 0)
+    return dgam + dbet + dW + [db]
+
+
+@pytest.mark.parametrize("widths,R", [
+    ((20, 200, 200, 200, 20), 20000),      # the lqr_d20 networks, many chunks
+    ((20, 200, 200, 200, 21), 777),        # Eikonal actor head, ragged rows
+    ((5, 256, 256, 256, 256, 1), 3001),    # 4 hidden layers at the width limit, critic V head
+    ((4, 7, 2), 1),                        # one row, tiny widths
+    ((10, 48, 130, 33, 10), 4099)])        # widths that split MFMA tiles and column groups
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_param_grads_vs_torch(widths, R, dtype):
+    scales, shifts, Ws, b = random_net(widths, dtype, seed=len(widths) + R)
+    g = torch.Generator().manual_seed(R)
+    rnd = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(dtype).to(DEV)
+    x = rnd(R, widths[0])
+    z = rnd(R, sum(widths[1:]))
+    G = rnd(R, sum(widths))
+    view = ops.MlpView(scales, shifts, Ws, b, False)
+    like = scales + shifts + Ws + [b]
+    rs = ops.bn_rs_host(dtype)
+    got = ops.mlp_param_grads(view, x, z, G, like)
+    ref = reference_grads(widths, scales, shifts, Ws, b, rs, x, z, G)
+    tol = 1e-11 if dtype == torch.float64 else 2e-5
+    for a, r in zip(got, ref):
+        assert a.shape == r.shape
+        err = float((a.double() - r).abs().max() / (1 + r.abs().max()))
+        assert err <= tol, (a.shape, err)
+
+
+def test_param_grads_strided_input_and_bad_args():
+    widths = (20, 64, 20)
+    scales, shifts, Ws, b = random_net(widths, torch.float64, seed=5)
+    R = 300
+    xfull = torch.randn(R, 32, dtype=torch.float64, device=DEV)
+    x = xfull[:, :20]  # row stride 32
+    z = torch.randn(R, 84, dtype=torch.float64, device=DEV)
+    G = torch.randn(R, 104, dtype=torch.float64, device=DEV)
+    view = ops.MlpView(scales, shifts, Ws, b, False)
+    like = scales + shifts + Ws + [b]
+    got = ops.mlp_param_grads(view, x, z, G, like)
+    ref = reference_grads(widths, scales, shifts, Ws, b, ops.bn_rs_host(torch.float64), x, z, G)
+    for a, r in zip(got, ref):
+        assert rel_close(a.cpu(), r.cpu(), 1e-11)
+    import ctypes
+    lib = _lib.load()
+    assert lib.dpac_mlp_param_grads(_lib.F64, 0, ctypes.byref(view.struct), 1.0, None, 20, None,
+                                    None, None, 0, None, None) == _lib.DPAC_EINVAL
+    ws = torch.empty(16, dtype=torch.uint8, device=DEV)
+    out = torch.empty(10, dtype=torch.float64, device=DEV)
+    rc = lib.dpac_mlp_param_grads(_lib.F64, R, ctypes.byref(view.struct), 1.0,
+                                  ctypes.c_void_p(x.data_ptr()), 32, ctypes.c_void_p(z.data_ptr()),
+                                  ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(ws.data_ptr()), 16,
+                                  ctypes.c_void_p(out.data_ptr()), None)
+    assert rc == _lib.DPAC_EINVAL and b"workspace too small" in lib.dpac_last_error()
+
+
+@pytest.mark.parametrize("name,d,hidden,dtype,tol", [
+    ("LQR", 20, (200, 200, 200), torch.float64, 1e-10), ("EKN", 5, (40, 40), torch.float64, 1e-10),
+    ("VDP", 10, (32, 48, 24), torch.float64, 1e-10), ("LQR", 20, (200, 200, 200), torch.float32, 1e-4)])
+def test_actor_bptt_param_grads_kernel_vs_torch(name, d, hidden, dtype, tol):
+    B, N, T = 300, 16, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme="adaptive",
+                      dtype="float64" if dtype == torch.float64 else "float32")
+    set_floatx("float64" if dtype == torch.float64 else "float32")
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net = psol.DeepNN(cfg, "actor", torch.Generator().manual_seed(9), dtype, DEV)
+    eqp = ep.params()
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=8, dtype=dtype, device=DEV)
+    grads = {}
+    try:
+        for mode in ("torch", "kernel"):
+            ops.PARAM_GRADS = mode
+            y, disc, xN = ops.actor_rollout_nn(eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, net)
+            grads[mode] = torch.autograd.grad(torch.mean(y + disc * torch.sum(xN * xN, 1)),
+                                              net.trainable_variables())
+    finally:
+        ops.PARAM_GRADS = "kernel"
+    for a, r in zip(grads["kernel"], grads["torch"]):
+        assert rel_close(a.cpu(), r.cpu(), tol)
