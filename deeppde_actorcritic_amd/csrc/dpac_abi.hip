@@ -24,6 +24,10 @@ int64_t mlp_param_grads_ws_bytes(int dtype, int64_t rows, const dpac_mlp& net);
 int mlp_param_grads_launch(int dtype, int64_t rows, const dpac_mlp& net, double gamma_scale,
                            const void* x, int64_t ldx, const void* z, const void* G, void* ws,
                            void* out, hipStream_t s);
+int mlp_rows_fwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx,
+                        void* out, void* save_z, hipStream_t s);
+int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
+                        const void* save_z, const void* g_out, void* G, void* g_x, hipStream_t s);
 
 namespace {
 thread_local std::string g_err;
@@ -410,6 +414,39 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
   return launch(a);
 }
 
+int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* x,
+                      int64_t ldx, void* out, void* save_z, void* stream) {
+  if (int e = check_net(net)) return e;
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
+  if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1 (got %lld)", (long long)rows);
+  if (ldx < net->width[0]) return fail(DPAC_EINVAL, "ldx (%lld) < width[0] (%d)", (long long)ldx,
+                                       net->width[0]);
+  for (int i = 0; i <= net->n_hidden; ++i)
+    if (!net->weight[i]) return fail(DPAC_EINVAL, "weight[%d] is NULL", i);
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(out);
+  const int r = mlp_rows_fwd_launch(dtype, rows, *net, x, ldx, out, save_z, (hipStream_t)stream);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
+}
+
+int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* const* weight_t,
+                      const void* save_z, const void* g_out, void* G, void* g_x, void* stream) {
+  if (int e = check_net(net)) return e;
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
+  if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1 (got %lld)", (long long)rows);
+  DPAC_REQUIRE(weight_t);
+  DPAC_REQUIRE(save_z);
+  DPAC_REQUIRE(g_out);
+  DPAC_REQUIRE(G);
+  for (int i = 0; i <= net->n_hidden; ++i)
+    if (!weight_t[i]) return fail(DPAC_EINVAL, "weight_t[%d] is NULL", i);
+  const int r = mlp_rows_bwd_launch(dtype, rows, *net, weight_t, save_z, g_out, G, g_x,
+                                    (hipStream_t)stream);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
+}
+
 int64_t dpac_mlp_param_grads_workspace(int32_t dtype, int64_t rows, const dpac_mlp* net) {
   if (check_net(net)) return -1;
   if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype), -1;
@@ -426,6 +463,13 @@ int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, doubl
   if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1 (got %lld)", (long long)rows);
   if (ldx < net->width[0]) return fail(DPAC_EINVAL, "ldx (%lld) < width[0] (%d)", (long long)ldx,
                                        net->width[0]);
+  {
+    int gtot = 0;
+    for (int i = 0; i <= net->n_hidden + 1; ++i) gtot += net->width[i];
+    if (ldx > gtot)
+      return fail(DPAC_EINVAL, "ldx (%lld) must not exceed the G row width (%d)", (long long)ldx,
+                  gtot);
+  }
   DPAC_REQUIRE(x);
   DPAC_REQUIRE(save_z);
   DPAC_REQUIRE(G);

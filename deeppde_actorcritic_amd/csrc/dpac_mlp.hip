@@ -4,6 +4,7 @@
 #include <algorithm>
 
 #include "dpac_mlp_grad.h"
+#include "dpac_mlp_rows.h"
 
 namespace dpac {
 
@@ -100,7 +101,70 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
   return (int)hipGetLastError();
 }
 
+template <typename T>
+MrArgs<T> mr_args(const dpac_mlp& net, int64_t rows) {
+  MrArgs<T> a{};
+  a.rows = rows;
+  a.L = net.n_hidden;
+  int zt = 0, gt = 0;
+  for (int i = 0; i <= a.L + 1; ++i) {
+    a.width[i] = net.width[i];
+    a.scale[i] = (const T*)net.bn_scale[i];
+    a.shift[i] = (const T*)net.bn_shift[i];
+    a.zoff[i] = i == 0 ? 0 : zt;
+    if (i > 0) zt += net.width[i];
+    a.goff[i] = gt;
+    gt += net.width[i];
+  }
+  for (int i = 0; i <= a.L; ++i) a.weight[i] = (const T*)net.weight[i];
+  a.bias = (const T*)net.bias;
+  a.ztot = zt;
+  a.gtot = gt;
+  return a;
+}
+
+template <typename T>
+int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void* out,
+             void* save_z, hipStream_t s) {
+  MrArgs<T> a = mr_args<T>(net, rows);
+  a.x = (const T*)x;
+  a.ldx = ldx;
+  a.out = (T*)out;
+  a.z = (T*)save_z;
+  constexpr int ROWS = MrCfg<T>::RT * 16;
+  hipLaunchKernelGGL(k_mlp_rows_fwd<T>, dim3((unsigned)((rows + ROWS - 1) / ROWS)),
+                     dim3(kMrThreads), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const void* save_z,
+             const void* g_out, void* G, void* g_x, hipStream_t s) {
+  MrArgs<T> a = mr_args<T>(net, rows);
+  for (int i = 0; i <= a.L; ++i) a.wt[i] = (const T*)wt[i];
+  a.z = (T*)save_z;
+  a.g_out = (const T*)g_out;
+  a.G = (T*)G;
+  a.g_x = (T*)g_x;
+  constexpr int ROWS = MrCfg<T>::RT * 16;
+  hipLaunchKernelGGL(k_mlp_rows_bwd<T>, dim3((unsigned)((rows + ROWS - 1) / ROWS)),
+                     dim3(kMrThreads), 0, s, a);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
+
+int mlp_rows_fwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx,
+                        void* out, void* save_z, hipStream_t s) {
+  return dtype == DPAC_F64 ? rows_fwd<double>(rows, net, x, ldx, out, save_z, s)
+                           : rows_fwd<float>(rows, net, x, ldx, out, save_z, s);
+}
+
+int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
+                        const void* save_z, const void* g_out, void* G, void* g_x, hipStream_t s) {
+  return dtype == DPAC_F64 ? rows_bwd<double>(rows, net, wt, save_z, g_out, G, g_x, s)
+                           : rows_bwd<float>(rows, net, wt, save_z, g_out, G, g_x, s);
+}
 
 int64_t mlp_param_grads_ws_bytes(int dtype, int64_t rows, const dpac_mlp& net) {
   return dtype == DPAC_F64 ? ws_bytes<double>(rows, net) : ws_bytes<float>(rows, net);

@@ -1,0 +1,296 @@
+// dpac_mlp_rows.h — a DeepNN (solver.py:227-278) over R independent rows, on
+// MFMA: the forward with the backward saves, and the backward's input-gradient
+// chain.  Used for the critic's V and G networks (solver.py:161-190), which the
+// reference evaluates per step inside the TD loop (solver.py:166-184) — here the
+// G network runs once over all N*B rows of the finished rollout.
+//
+// Workgroup = 4 wavefronts over RT*16 consecutive rows.  Every dense layer is an
+// [RT*16 x K] x [K x H] product: the waves split the 16-column tiles, each wave
+// keeps RT x NT accumulator tiles, B fragments (the weights, L2-resident) stream
+// through an 8-deep register ring shared by the RT row tiles, A fragments come
+// from the LDS image of the layer input.  Activations never leave LDS between
+// layers; the epilogues apply BN / y + relu(y) (forward) or the activation
+// factor (backward) and write the saves / G rows.
+#pragma once
+
+#include "dpac_device.h"
+
+namespace dpac {
+
+constexpr int kMrThreads = 256;
+constexpr int kMrWaves = 4;
+constexpr int kMrLd = DPAC_MLP_MAX_WIDTH + 4;  // LDS row stride: 16 rows x 4 k hit 64 banks
+constexpr int kMrPrefetch = 8;
+
+template <typename T>
+struct MrCfg;
+template <>
+struct MrCfg<float> {
+  static constexpr int RT = 4;  // 64 rows per workgroup
+};
+template <>
+struct MrCfg<double> {
+  static constexpr int RT = 2;
+};
+
+template <typename T>
+struct MrArgs {
+  int64_t rows;
+  int L;
+  int width[DPAC_MLP_MAX_HIDDEN + 2];
+  const T* scale[DPAC_MLP_MAX_HIDDEN + 2];
+  const T* shift[DPAC_MLP_MAX_HIDDEN + 2];
+  const T* weight[DPAC_MLP_MAX_HIDDEN + 1];  // forward: W_i [w_i][w_{i+1}]
+  const T* wt[DPAC_MLP_MAX_HIDDEN + 1];      // backward: (W_i diag s_{i+1})^T [w_{i+1}][w_i]
+  const T* bias;
+  int zoff[DPAC_MLP_MAX_HIDDEN + 2], goff[DPAC_MLP_MAX_HIDDEN + 2];
+  int ztot, gtot;
+  const T* x;      // [rows][ldx]
+  int64_t ldx;
+  T* out;          // [rows][w_{L+1}]
+  T* z;            // saves [rows][ztot] (forward: optional output; backward: input)
+  const T* g_out;  // backward: dL/d out [rows][w_{L+1}]
+  T* G;            // backward: [rows][gtot]
+  T* g_x;          // backward, optional: dL/dx [rows][w_0]
+};
+
+// acc[RT][NT] = in[RT*16 x K] @ W[K x Nout] for this wave's NT column tiles
+// (wave, wave + 4, ...), then epi.template finish<NT>(acc).  `in` is an LDS
+// [RT*16][kMrLd] image whose columns past K hold finite values (the B rows past
+// K read 0 through the descriptor, so they add nothing).
+template <typename T, int NT, int RT, class EPI>
+__device__ __forceinline__ void mr_layer_nt(const T* in, int K, int Nout, const T* W, int wave,
+                                            int lane, EPI& epi) {
+  using MF = Mfma<T>;
+  const int col_l = lane & 15, kq = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, (uint32_t)(K * Nout * (int)sizeof(T)));
+  uint32_t voff[NT];
+  typename MF::acc_t acc[RT][NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kMrWaves * j) * 16 + col_l;
+    voff[j] = col < Nout ? (uint32_t)((kq * Nout + col) * (int)sizeof(T)) : kOOB;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt][j] = typename MF::acc_t{0, 0, 0, 0};
+  }
+  const uint32_t kstep_bytes = (uint32_t)(4 * Nout * (int)sizeof(T));
+  const int nks = (K + 3) / 4;
+  const T* arow = in + col_l * kMrLd + kq;
+  auto loadB = [&](int ks, int j) {
+    uint32_t w[sizeof(T) / 4];
+    buf_load_dwords<sizeof(T) / 4>(rW, voff[j] + (uint32_t)ks * kstep_bytes, w);
+    T v;
+    __builtin_memcpy(&v, &w[0], sizeof(T));
+    return v;
+  };
+  auto loadA = [&](int ks, int rt) { return arow[rt * 16 * kMrLd + 4 * (ks < nks ? ks : nks - 1)]; };
+  T bq[kMrPrefetch][NT], av[kMrPrefetch][RT];
+#pragma unroll
+  for (int q = 0; q < kMrPrefetch; ++q) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) av[q][rt] = loadA(q, rt);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bq[q][j] = loadB(q, j);
+  }
+  for (int ks0 = 0; ks0 < nks; ks0 += kMrPrefetch) {
+    T an[kMrPrefetch][RT];
+#pragma unroll
+    for (int q = 0; q < kMrPrefetch; ++q)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) an[q][rt] = loadA(ks0 + kMrPrefetch + q, rt);
+#pragma unroll
+    for (int q = 0; q < kMrPrefetch; ++q) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = MF::mma(av[q][rt], bq[q][j], acc[rt][j]);
+        bq[q][j] = loadB(ks0 + q + kMrPrefetch, j);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kMrPrefetch; ++q)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) av[q][rt] = an[q][rt];
+  }
+  epi.template finish<NT>(acc, wave, lane);
+}
+
+template <typename T, int RT, class EPI>
+__device__ __forceinline__ void mr_layer(const T* in, int K, int Nout, const T* W, int wave,
+                                         int lane, EPI& epi) {
+  const int ntiles = (Nout + 15) / 16;
+  const int mine = ntiles > wave ? (ntiles - wave + kMrWaves - 1) / kMrWaves : 0;
+  static_assert(DPAC_MLP_MAX_WIDTH / 16 / kMrWaves == 4, "dispatch below covers 1..4 tiles");
+  switch (mine) {
+    case 1: mr_layer_nt<T, 1, RT>(in, K, Nout, W, wave, lane, epi); break;
+    case 2: mr_layer_nt<T, 2, RT>(in, K, Nout, W, wave, lane, epi); break;
+    case 3: mr_layer_nt<T, 3, RT>(in, K, Nout, W, wave, lane, epi); break;
+    case 4: mr_layer_nt<T, 4, RT>(in, K, Nout, W, wave, lane, epi); break;
+    default: break;
+  }
+}
+
+// Forward epilogue of dense layer l (output width Nout): z -> save -> BN(z (+ b))
+// -> [y + relu(y)] into the next LDS image, or (output layer) to `out`.
+template <typename T, int RT>
+struct MrFwdEpi {
+  const T *scale, *shift, *bias;  // BN_{l+1}; bias only for the output layer
+  bool hidden;
+  int Nout, rows_live;
+  T* lds;           // next layer's input image
+  T* save;          // z of row 0 of the workgroup at this layer's column offset, or null
+  int64_t save_ld;
+  T* out;           // output layer: out row 0 of the workgroup
+  int64_t out_ld;
+  template <int NT>
+  __device__ void finish(typename Mfma<T>::acc_t (&acc)[RT][NT], int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = (wave + kMrWaves * j) * 16 + (lane & 15);
+      const bool valid = col < Nout;
+      const T s = valid ? scale[col] : T(0), sh = valid ? shift[col] : T(0);
+      const T bb = (valid && bias) ? bias[col] : T(0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = rt * 16 + Mfma<T>::row(lane, i);
+          const T zv = acc[rt][j][i];
+          const bool st = valid && row < rows_live;
+          if (save && st) save[row * save_ld + col] = zv;
+          T yv = bias ? zv + bb : zv;   // addmm(b, y, W) (solver.py:270)
+          yv = sh + yv * s;              // addcmul(beta, y, gamma/sqrt(1+eps))
+          if (hidden) {
+            yv = yv + fmax(yv, T(0));    // y + relu(y) (solver.py:269)
+            lds[row * kMrLd + col] = valid ? yv : T(0);
+          } else if (st) {
+            out[row * out_ld + col] = yv;
+          }
+        }
+      }
+    }
+  }
+};
+
+// Backward epilogue of the input-gradient product g = G_{l+1} @ (W_l diag s_{l+1})^T
+// (output width Nout = w_l): for l >= 1 times the activation factor 1 + [y_l > 0]
+// (y_l = BN_l(z_l), z_l from the saves), then G_l to global and to LDS.
+template <typename T, int RT>
+struct MrBwdEpi {
+  const T *scale, *shift;  // BN_l, or null for l == 0
+  const T* z;              // z_l of row 0 of the workgroup (l >= 1)
+  int64_t z_ld;
+  int Nout, rows_live;
+  T* lds;
+  T* g;                    // G_l of row 0 of the workgroup
+  int64_t g_ld;
+  template <int NT>
+  __device__ void finish(typename Mfma<T>::acc_t (&acc)[RT][NT], int wave, int lane) {
+    T zz[NT][RT][4];
+    if (scale) {  // all the z loads first, then the stores
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = (wave + kMrWaves * j) * 16 + (lane & 15);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = rt * 16 + Mfma<T>::row(lane, i);
+            zz[j][rt][i] = (col < Nout && row < rows_live) ? z[row * z_ld + col] : T(0);
+          }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = (wave + kMrWaves * j) * 16 + (lane & 15);
+      const bool valid = col < Nout;
+      const T s = (scale && valid) ? scale[col] : T(0), sh = (scale && valid) ? shift[col] : T(0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = rt * 16 + Mfma<T>::row(lane, i);
+          T v = acc[rt][j][i];
+          if (scale) {
+            const T yv = sh + zz[j][rt][i] * s;     // the forward's BN_l output
+            v = v * (yv > T(0) ? T(2) : T(1));      // d(y + relu(y))/dy
+          }
+          if (valid && row < rows_live) g[row * g_ld + col] = v;
+          lds[row * kMrLd + col] = valid ? v : T(0);
+        }
+      }
+    }
+  }
+};
+
+template <typename T>
+__global__ __launch_bounds__(kMrThreads) void k_mlp_rows_fwd(const MrArgs<T> a) {
+  constexpr int RT = MrCfg<T>::RT, ROWS = RT * 16;
+  __shared__ T s_img[2][ROWS * kMrLd];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+  const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
+  const int d = a.width[0];
+  // a_0 = BN_0(x) into image 0 (solver.py:265); everything else zero
+  for (int e = tid; e < ROWS * kMrLd; e += kMrThreads) {
+    const int r = e / kMrLd, k = e % kMrLd;
+    T v = T(0);
+    if (k < d && r < rows_live) v = a.shift[0][k] + a.x[(row0 + r) * a.ldx + k] * a.scale[0][k];
+    s_img[0][e] = v;
+    s_img[1][e] = T(0);
+  }
+  __syncthreads();
+  int pq = 0;
+  for (int l = 0; l <= a.L; ++l) {
+    const int Nout = a.width[l + 1];
+    MrFwdEpi<T, RT> epi{a.scale[l + 1], a.shift[l + 1], l == a.L ? a.bias : nullptr, l < a.L,
+                        Nout, rows_live, s_img[pq ^ 1],
+                        a.z ? a.z + row0 * a.ztot + a.zoff[l + 1] : nullptr, a.ztot,
+                        a.out + row0 * Nout, Nout};
+    mr_layer<T, RT>(s_img[pq], a.width[l], Nout, a.weight[l], wave, lane, epi);
+    __syncthreads();
+    pq ^= 1;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kMrThreads) void k_mlp_rows_bwd(const MrArgs<T> a) {
+  constexpr int RT = MrCfg<T>::RT, ROWS = RT * 16;
+  __shared__ T s_img[2][ROWS * kMrLd];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+  const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
+  const int L = a.L, hout = a.width[L + 1];
+  // G_{L+1} = dL/d out: into image 0 and to G
+  for (int e = tid; e < ROWS * kMrLd; e += kMrThreads) {
+    const int r = e / kMrLd, k = e % kMrLd;
+    T v = T(0);
+    if (k < hout && r < rows_live) {
+      v = a.g_out[(row0 + r) * hout + k];
+      a.G[(row0 + r) * a.gtot + a.goff[L + 1] + k] = v;
+    }
+    s_img[0][e] = v;
+    s_img[1][e] = T(0);
+  }
+  __syncthreads();
+  int pq = 0;
+  for (int l = L; l >= 0; --l) {
+    MrBwdEpi<T, RT> epi{l >= 1 ? a.scale[l] : nullptr, l >= 1 ? a.shift[l] : nullptr,
+                        a.z + row0 * a.ztot + a.zoff[l], a.ztot, a.width[l], rows_live,
+                        s_img[pq ^ 1], a.G + row0 * a.gtot + a.goff[l], a.gtot};
+    mr_layer<T, RT>(s_img[pq], a.width[l + 1], a.width[l], a.wt[l], wave, lane, epi);
+    __syncthreads();
+    pq ^= 1;
+  }
+  if (a.g_x) {  // dL/dx = G_0 * s_0 (a_0 = beta_0 + x * s_0)
+    const int d = a.width[0];
+    for (int e = tid; e < rows_live * d; e += kMrThreads) {
+      const int r = e / d, k = e % d;
+      a.g_x[(row0 + r) * d + k] = s_img[pq][r * kMrLd + k] * a.scale[0][k];
+    }
+  }
+}
+
+}  // namespace dpac

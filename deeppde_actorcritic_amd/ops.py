@@ -367,6 +367,80 @@ def actor_rollout_nn(eqp, scheme: int, x0, dw, total_time: float, num_steps: int
                                  *net.trainable_variables())
 
 
+# "kernel": DeepNN on independent rows runs dpac_mlp_rows_fwd/bwd + dpac_mlp_param_grads;
+# "torch": PyTorch GEMMs and autograd (test reference).
+ROW_MLP = "kernel"
+
+
+def _split_params(params):
+    L = (len(params) - 1) // 3 - 1
+    return L, params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
+
+
+def mlp_rows(view: MlpView, x: torch.Tensor, save: bool = False):
+    """out [R, w_out] (the network before any Eikonal head) for every row of x [R, d],
+    one dpac_mlp_rows_fwd launch; with save=True also z [R, Σ widths[1:]]."""
+    _require_gpu(x, *view.tensors)
+    _check_same(x, *view.tensors)
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("mlp_rows: x must be [rows, d] with unit column stride")
+    R = x.shape[0]
+    out = torch.empty(R, view.widths[-1], dtype=x.dtype, device=x.device)
+    z = torch.empty(R, sum(view.widths[1:]), dtype=x.dtype, device=x.device) if save else None
+    call("dpac_mlp_rows_fwd", _dtype_id(x), R, ctypes.byref(view.struct),
+         ctypes.c_void_p(x.data_ptr()), x.stride(0), _ptr(out), _ptr(z), _stream(x))
+    return out, z
+
+
+class _RowMLP(torch.autograd.Function):
+    """DeepNN (solver.py:260-271, before the Eikonal head) over independent rows with
+    the hand-written kernels: forward = dpac_mlp_rows_fwd with saves; backward =
+    dpac_mlp_rows_bwd (input-gradient chain, G of every BN output, dL/dx) +
+    dpac_mlp_param_grads.  Inputs: x [R, d], rs, DeepNN.trainable_variables()."""
+
+    @staticmethod
+    def forward(ctx, x, rs, *params):
+        L, gam, bet, Ws, b = _split_params(params)
+        view = MlpView([rs * g for g in gam], bet, Ws, b, False)
+        need = any(ctx.needs_input_grad)
+        out, z = mlp_rows(view, x, save=need)
+        if need:
+            ctx.save_for_backward(x, z, rs, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        x, z, rs, *params = ctx.saved_tensors
+        L, gam, bet, Ws, b = _split_params(params)
+        s = [rs * g for g in gam]
+        view = MlpView(s, bet, Ws, b, False)
+        R = x.shape[0]
+        wt = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]
+        wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
+        G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
+        g_x = torch.empty(R, view.widths[0], dtype=x.dtype, device=x.device) \
+            if ctx.needs_input_grad[0] else None
+        call("dpac_mlp_rows_bwd", _dtype_id(x), R, ctypes.byref(view.struct), wt_ptrs, _ptr(z),
+             _ptr(g_out.contiguous()), _ptr(G), _ptr(g_x), _stream(x))
+        grads = [None] * len(params)
+        if any(ctx.needs_input_grad[2:]):
+            grads = mlp_param_grads(view, x, z, G, params)
+        return (g_x, None, *grads)
+
+
+def row_mlp(net, x: torch.Tensor) -> torch.Tensor:
+    """net(x) before the Eikonal head, x [..., d] -> [..., w_out], through the kernels."""
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(1) != 1:
+        x2 = x2.contiguous()
+    if torch.is_grad_enabled() and (x2.requires_grad or any(p.requires_grad for p in net.trainable_variables())):
+        out = _RowMLP.apply(x2, net.bn_rs, *net.trainable_variables())
+    else:
+        out, _ = mlp_rows(net.mlp_view(), x2)
+    return out.reshape(*lead, out.shape[-1])
+
+
 def flag_init(eqp, scheme: int, x0: torch.Tensor, total_time: float, num_steps: int):
     _require_gpu(x0)
     flag = torch.empty(x0.shape[0], dtype=torch.int32, device=x0.device)

@@ -82,6 +82,9 @@ class DeepNN(nn.Module):
         all N steps): then every product is a batched GEMM over S with the weight
         broadcast, so autograd forms the weight gradients as S partial products and
         a sum instead of one GEMM with a 10^5-long reduction."""
+        if x.is_cuda and ops.ROW_MLP == "kernel" and self.fused_ok():
+            y = ops.row_mlp(self, x)  # hand-written MFMA kernels (dpac_mlp_rows_*)
+            return self._ekn(y) if self.ekn_head else y
         rs = self.bn_rs
         g, bt, W = self.bn_gamma, self.bn_beta, self.W
         L = len(self.sizes) - 2
@@ -98,11 +101,13 @@ class DeepNN(nn.Module):
             y = y + torch.relu(y)
         y = mm_bias(self.b, y, W[L])
         y = torch.addcmul(bt[L + 1], y, rs * g[L + 1])
-        if self.ekn_head:  # solver.py:272-274
-            d = self.d
-            norm_y = torch.sum(y[..., 0:d] ** 2, -1, keepdim=True) ** 0.5
-            y = y[..., 0:d] / (1e-15 + torch.relu(y[..., d:d + 1]) + norm_y)
-        return y
+        return self._ekn(y) if self.ekn_head else y
+
+    def _ekn(self, y):
+        """The Eikonal actor head, solver.py:272-274."""
+        d = self.d
+        norm_y = torch.sum(y[..., 0:d] ** 2, -1, keepdim=True) ** 0.5
+        return y[..., 0:d] / (1e-15 + torch.relu(y[..., d:d + 1]) + norm_y)
 
     def fused_ok(self) -> bool:
         """Whether dpac_rollout_nn_fwd can run this network (layer and width limits)."""

@@ -271,12 +271,29 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
                         const int32_t* save_flag, const void* save_disc, const void* g_xN,
                         const void* g_disc, const void* g_y, void* G, void* g_x0, void* stream);
 
+/* ---- a dpac_mlp over independent rows (the critic's networks) -------------
+ * Forward: out [rows][width[n_hidden+1]] = the network (bn_0 -> (dense -> bn ->
+ * y+relu(y)) x n_hidden -> dense(+bias) -> bn_last, solver.py:260-271) applied to
+ * every row of x (row stride ldx), on MFMA tiles.  ekn_head is ignored: `out` is
+ * the network output before the Eikonal head (solver.py:272-274).  save_z
+ * (optional) [rows][Σ_{i>=1} width[i]]: the pre-BN output of every dense layer,
+ * as dpac_rollout_nn_fwd saves it.  Replaces DeepNN.call (solver.py:260-278) for
+ * NN_value / NN_value_grad on the TD loop's states (solver.py:161-190).
+ * Backward: given g_out [rows][width[n_hidden+1]] (dL/d out) and the forward's
+ * save_z, writes G [rows][Σ_i width[i]], block i = dL/d(output of BN_i) — the
+ * input of dpac_mlp_param_grads — and optionally g_x [rows][width[0]] = dL/dx.
+ * weight_t[i] = (weight[i] * bn_scale[i+1])^T, [width[i+1]][width[i]] row-major. */
+int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* x,
+                      int64_t ldx, void* out, void* save_z, void* stream);
+int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* const* weight_t,
+                      const void* save_z, const void* g_out, void* G, void* g_x, void* stream);
+
 /* ---- parameter gradients of a dpac_mlp over independent rows -------------
  * What GradientTape returns for DeepNN's trainable variables (solver.py:88,95
  * through solver.py:260-271), given the backward chain's G [rows][Σ_i width[i]]
  * (as written by dpac_rollout_nn_bwd or dpac_mlp_rows_bwd) and the forward's
  * save_z [rows][Σ_{i>=1} width[i]]; x [rows] with row stride ldx is the network
- * input.  With s_i = bn_scale[i], a_0 = bn_shift[0] + x*s_0 and
+ * input (ldx <= Σ_i width[i]).  With s_i = bn_scale[i], a_0 = bn_shift[0] + x*s_0 and
  * a_i = y_i + relu(y_i), y_i = bn_shift[i] + z_i*s_i:
  *   dW_i = Σ_r a_i^T (G_{i+1} ⊙ s_{i+1}),  dbeta_i = Σ_r G_i,
  *   dgamma_i = gamma_scale · Σ_r G_i ⊙ zin_i  (zin_0 = x, zin_{L+1} = z_{L+1} + bias),

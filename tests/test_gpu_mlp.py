@@ -132,3 +132,90 @@ def test_actor_bptt_param_grads_kernel_vs_torch(name, d, hidden, dtype, tol):
         ops.PARAM_GRADS = "kernel"
     for a, r in zip(grads["kernel"], grads["torch"]):
         assert rel_close(a.cpu(), r.cpu(), tol)
+
+
+# ---------------------------------------------------------------------------
+# dpac_mlp_rows_fwd / _bwd: DeepNN over independent rows (the critic's V and G
+# networks) against the PyTorch statement of the same network.
+# ---------------------------------------------------------------------------
+def net_pair(AC, name, d, hidden, dtype, seed=4):
+    cfg = full_config(name, d, hidden=hidden, dtype="float64" if dtype == torch.float64 else "float32")
+    set_floatx("float64" if dtype == torch.float64 else "float32")
+    return psol.DeepNN(cfg, AC, torch.Generator().manual_seed(seed), dtype, DEV)
+
+
+def torch_path(fn):
+    try:
+        ops.ROW_MLP = "torch"
+        return fn()
+    finally:
+        ops.ROW_MLP = "kernel"
+
+
+ROW_CASES = [("critic_grad", "LQR", 20, (200, 200, 200), 20000), ("critic", "LQR", 20, (200, 200, 200), 6144),
+             ("critic", "VDP", 4, (256, 256, 256, 256), 1), ("actor", "EKN", 5, (40, 7), 333),
+             ("critic_grad", "LQR_var", 10, (48, 130, 33), 4099)]
+
+
+@pytest.mark.parametrize("AC,name,d,hidden,R", ROW_CASES)
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_row_mlp_forward_and_saves(AC, name, d, hidden, R, dtype):
+    net = net_pair(AC, name, d, hidden, dtype)
+    x = torch.randn(R, d, dtype=dtype, device=DEV, generator=torch.Generator(DEV).manual_seed(R)) * 0.5
+    with torch.no_grad():
+        got = net(x)
+        ref = torch_path(lambda: net(x))
+        out, z = ops.mlp_rows(net.mlp_view(), x, save=True)
+    tol = 1e-12 if dtype == torch.float64 else 2e-5
+    assert got.shape == ref.shape
+    assert rel_close(got.cpu(), ref.cpu(), tol)
+    # the saves are the pre-BN dense outputs: recompute layer by layer in PyTorch
+    rs, g, bt, W = net.bn_rs, net.bn_gamma, net.bn_beta, net.W
+    y = torch.addcmul(bt[0], x, rs * g[0])
+    zs, L = [], len(net.sizes) - 2
+    for i in range(L + 1):
+        zi = y @ W[i]
+        zs.append(zi)
+        y = torch.addcmul(bt[i + 1], zi if i < L else zi + net.b, rs * g[i + 1])
+        if i < L:
+            y = y + torch.relu(y)
+    assert rel_close(z.cpu(), torch.cat(zs, 1).detach().cpu(), 1e-11 if dtype == torch.float64 else 1e-4)
+
+
+@pytest.mark.parametrize("AC,name,d,hidden,R", ROW_CASES)
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_row_mlp_gradients(AC, name, d, hidden, R, dtype):
+    net = net_pair(AC, name, d, hidden, dtype)
+    gen = torch.Generator(DEV).manual_seed(R + 1)
+    x = (torch.randn(R, d, dtype=dtype, device=DEV, generator=gen) * 0.5).requires_grad_(True)
+    wgt = torch.randn(R, net.sizes[-1] - (1 if net.ekn_head else 0), dtype=dtype, device=DEV, generator=gen)
+
+    def grads():
+        loss = torch.sum(net(x) * wgt) / R
+        return torch.autograd.grad(loss, [x] + net.trainable_variables())
+
+    got = grads()
+    ref = torch_path(grads)
+    tol = 1e-10 if dtype == torch.float64 else 1e-4
+    for a, r in zip(got, ref):
+        assert a.shape == r.shape
+        scale = float(r.abs().max())
+        assert float((a - r).abs().max()) <= tol * (1 + scale)
+
+
+def test_row_mlp_stacked_input_and_errors():
+    """[S, R, d] input (the critic's G over all N steps) and argument checks."""
+    net = net_pair("critic_grad", "LQR", 5, (24, 40), torch.float64)
+    x = torch.randn(7, 33, 5, dtype=torch.float64, device=DEV)
+    with torch.no_grad():
+        got = net(x)
+        ref = torch_path(lambda: net(x))
+    assert got.shape == (7, 33, 5) and rel_close(got.cpu(), ref.cpu(), 1e-12)
+    import ctypes
+    lib = _lib.load()
+    view = net.mlp_view()
+    assert lib.dpac_mlp_rows_fwd(_lib.F64, 10, ctypes.byref(view.struct), None, 5, None, None,
+                                 None) == _lib.DPAC_EINVAL
+    assert lib.dpac_mlp_rows_fwd(_lib.F64, 10, ctypes.byref(view.struct),
+                                 ctypes.c_void_p(x.data_ptr()), 3, ctypes.c_void_p(x.data_ptr()),
+                                 None, None) == _lib.DPAC_EINVAL  # ldx < d
