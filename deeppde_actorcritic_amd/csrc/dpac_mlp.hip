@@ -46,11 +46,12 @@ PgArgs<T> pg_args(const dpac_mlp& net, int64_t rows, const void* x, int64_t ldx,
 
 template <typename T>
 int64_t pg_chunk_rows(int64_t rows, int64_t max_ld) {
-  // ~192 chunks: 4-8 workgroups per CU over the (group, layer) grid, and a
-  // partial buffer the reduce reads in ~10 us.  A chunk's rows are addressed
+  // 128 chunks: the wide layers' two column groups give 256 workgroups, one per
+  // CU (the kernel holds a CU alone at ~300 registers per lane), and a partial
+  // buffer the reduce reads in a few microseconds.  A chunk's rows are addressed
   // through 32-bit buffer descriptors: keep them below 2 GiB.
   constexpr int SR = PgCfg<T>::SR;
-  int64_t per = (rows + 191) / 192;
+  int64_t per = (rows + 127) / 128;
   const int64_t cap = (((int64_t)1 << 31) - 1) / (max_ld * (int64_t)sizeof(T)) / SR * SR;
   per = (per + SR - 1) / SR * SR;
   return std::max<int64_t>(std::min(per, cap), SR);
@@ -76,25 +77,38 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
   a.rows_per_chunk = pg_chunk_rows<T>(rows, max_ld(a));
   a.part = (T*)ws;
   const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
-  int maxw = 0;
-  for (int i = 1; i <= a.L + 1; ++i) maxw = std::max(maxw, a.width[i]);
-  constexpr int CW = 64 * PgCfg<T>::NTJ;
-  // one launch per layer: the row-tile count of dW_l (ceil(width[l]/16)) is a
-  // template bin, 1 / 2 / 4 / 8 / 13 / 16
+  // one launch per layer: the wave grid and the tile counts are template bins
+  // (wide layers: 1 x 4 waves, 2 column tiles each (f64: 1), row tiles
+  // 1/2/4/8/13/16; layers of <= 32 outputs: 4 x 1 waves over the row tiles)
   for (int l = 0; l <= a.L; ++l) {
-    const int nti = (a.width[l] + 15) / 16;
-    const dim3 grid((unsigned)nch, (unsigned)((a.width[l + 1] + CW - 1) / CW));
-#define DPAC_PG(NT) hipLaunchKernelGGL((k_param_grads<T, NT>), grid, dim3(kPgThreads), 0, s, a, l)
-    if (nti <= 1) DPAC_PG(1);
-    else if (nti <= 2) DPAC_PG(2);
-    else if (nti <= 4) DPAC_PG(4);
-    else if (nti <= 8) DPAC_PG(8);
-    else if (nti <= 13) DPAC_PG(13);
-    else DPAC_PG(16);
+    const int K = a.width[l], H = a.width[l + 1];
+    const int nti = (K + 15) / 16;
+    if (H <= 32) {
+      const int ntj = (H + 15) / 16, nt4 = (nti + 3) / 4;
+      const dim3 grid((unsigned)nch, 1u);
+#define DPAC_PGN(NI, NJ) hipLaunchKernelGGL((k_param_grads<T, NI, NJ, 4>), grid, dim3(kPgThreads), 0, s, a, l)
+#define DPAC_PGN_J(NI) if (ntj == 1) DPAC_PGN(NI, 1); else DPAC_PGN(NI, 2);
+      if (nt4 <= 1) { DPAC_PGN_J(1) }
+      else if (nt4 <= 2) { DPAC_PGN_J(2) }
+      else if (nt4 <= 3) { DPAC_PGN_J(3) }
+      else { DPAC_PGN_J(4) }
+#undef DPAC_PGN_J
+#undef DPAC_PGN
+    } else {
+      constexpr int NJ = sizeof(T) == 4 ? 2 : 1;
+      constexpr int CW = 16 * NJ * 4;
+      const dim3 grid((unsigned)nch, (unsigned)((H + CW - 1) / CW));
+#define DPAC_PG(NI) hipLaunchKernelGGL((k_param_grads<T, NI, NJ, 1>), grid, dim3(kPgThreads), 0, s, a, l)
+      if (nti <= 1) DPAC_PG(1);
+      else if (nti <= 2) DPAC_PG(2);
+      else if (nti <= 4) DPAC_PG(4);
+      else if (nti <= 8) DPAC_PG(8);
+      else if (nti <= 13) DPAC_PG(13);
+      else DPAC_PG(16);
 #undef DPAC_PG
+    }
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
-  (void)maxw;
   const int64_t n = a.ptot + a.width[a.L + 1];
   hipLaunchKernelGGL(k_param_grads_reduce<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                      a, (int)nch, (T)gamma_scale, (T*)out);

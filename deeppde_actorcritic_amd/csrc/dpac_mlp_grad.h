@@ -26,18 +26,12 @@
 namespace dpac {
 
 constexpr int kPgThreads = 256;
-constexpr int kPgMaxTiles = DPAC_MLP_MAX_WIDTH / 16;
 constexpr int kPgQ = DPAC_MLP_MAX_WIDTH / 64;  // A-stage columns per thread
 
+// Rows staged per sub-chunk (4 row phases of the 4 wavefronts).
 template <typename T>
-struct PgCfg;
-template <>
-struct PgCfg<float> {
-  static constexpr int NTJ = 2, SR = 16;  // 128 accumulator registers (AGPRs)
-};
-template <>
-struct PgCfg<double> {
-  static constexpr int NTJ = 1, SR = 16;
+struct PgCfg {
+  static constexpr int SR = 16;
 };
 
 template <typename T>
@@ -68,24 +62,33 @@ __device__ __forceinline__ T buf_load_elem(__amdgpu_buffer_rsrc_t r, uint32_t vo
 }
 
 // One sub-chunk's global loads, issued before the MFMA phase of the previous one.
-template <typename T, int SR, int NTJ>
+template <typename T, int SR, int QB>
 struct PgStage {
-  T a[SR / 4][kPgQ];   // zin_l (A source) at rows wave + 4m, columns lane + 64q
-  T g0[SR / 4];        // layer 0 only: G_0 at column lane (BN_0 sums)
-  T gb[SR / 4][NTJ];   // G_{l+1} at columns col0 + lane + 64q
-  T zb[SR / 4][NTJ];   // zin_{l+1} (pre-bias) at the same places
+  T a[SR / 4][kPgQ];  // zin_l (A source) at rows wave + 4m, columns lane + 64q
+  T g0[SR / 4];       // layer 0 only: G_0 at column lane (BN_0 sums)
+  T gb[SR / 4][QB];   // G_{l+1} at columns col0 + lane + 64q
+  T zb[SR / 4][QB];   // zin_{l+1} (pre-bias) at the same places
 };
 
-// Workgroup (chunk c, column group g, layer l): the chunk's partial of dW_l for
-// B columns [g*CW, (g+1)*CW), plus the BN_{l+1} column sums of those columns
-// (and, layer 0 / group 0, the BN_0 sums).
-template <typename T, int NTI>
+// Workgroup (chunk c, column group g) of layer l: the chunk's partial of dW_l
+// for B columns [g*CW, (g+1)*CW), plus the BN_{l+1} column sums of those
+// columns (and, layer 0 / group 0, the BN_0 sums).  The 4 wavefronts form a
+// WI x WJ grid over the output tiles: wave (wi, wj) owns row tiles wi + WI*m
+// (m < NTI) and column tiles wj + WJ*j (j < NTJ), so NTI*WI*16 >= K and
+// CW = NTJ*WJ*16.  Wide layers use WI = 1, WJ = 4; the narrow output layer
+// (H <= 32) WI = 4, WJ = 1, so no wavefront multiplies padding columns.
+// NTI / NTJ are compile-time: the MFMA loop is straight-line code.
+template <typename T, int NTI, int NTJ, int WI>
 __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, const int l) {
   using MF = Mfma<T>;
-  constexpr int NTJ = PgCfg<T>::NTJ, SR = PgCfg<T>::SR;
-  constexpr int CW = 64 * NTJ;                     // B columns per workgroup
-  constexpr int LDA = DPAC_MLP_MAX_WIDTH + 16;     // row strides: lanes of a k-quad
-  constexpr int LDB = CW + 16;                     // land 16 words apart
+  constexpr int WJ = 4 / WI;
+  constexpr int SR = PgCfg<T>::SR;
+  constexpr int CW = 16 * NTJ * WJ;               // B columns per workgroup
+  constexpr int QB = (CW + 63) / 64;              // B columns per thread
+  constexpr int LDA = DPAC_MLP_MAX_WIDTH + 16;    // row strides: lanes of a k-quad
+  constexpr int LDB = (CW < 64 ? 64 : CW) + 16;   // land 16 words apart
+  constexpr int kpad = 16 * NTI * WI;             // staged A columns
+  static_assert(kpad <= DPAC_MLP_MAX_WIDTH, "A image");
   constexpr uint32_t ES = sizeof(T);
   __shared__ T sA[SR * LDA];
   __shared__ T sB[SR * LDB];
@@ -93,10 +96,9 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
   const int K = a.width[l], H = a.width[l + 1];
   const int col0 = grp * CW;
   if (col0 >= H) return;  // whole workgroup: no barrier reached yet
-  // NTI >= ceil(K/16) row tiles (a compile-time count: the MFMA loop is
-  // straight-line code); tiles past K multiply zero padding
   const int tid = threadIdx.x, lane = tid % 64;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64);
+  const int wi = wave / WJ, wj = wave % WJ;
   const int64_t chunk = blockIdx.x;
   const int64_t r_begin = chunk * a.rows_per_chunk;
   const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
@@ -107,11 +109,10 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
   const T* gA = a.G + a.goff[0];
   const T* gB = a.G + a.goff[l + 1] + col0;
   const T* zB = a.z + a.zoff[l + 1] + col0;
-  constexpr int kpad = 16 * NTI;
 
   // per-thread constants: A columns lane + 64q, B columns col0 + lane + 64q
-  T sa[kPgQ], ha[kPgQ], sbv[NTJ], bbv[NTJ];
-  uint32_t offA[kPgQ], offB[NTJ];
+  T sa[kPgQ], ha[kPgQ], sbv[QB], bbv[QB];
+  uint32_t offA[kPgQ], offB[QB];
 #pragma unroll
   for (int q = 0; q < kPgQ; ++q) {
     const int k = lane + 64 * q;
@@ -120,16 +121,17 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
     offA[q] = k < K ? (uint32_t)k * ES : kOOB;
   }
 #pragma unroll
-  for (int q = 0; q < NTJ; ++q) {
-    const int h = col0 + lane + 64 * q;
-    sbv[q] = h < H ? a.scale[l + 1][h] : T(0);
-    bbv[q] = (h < H && last) ? a.bias[h] : T(0);
-    offB[q] = h < H ? (uint32_t)(lane + 64 * q) * ES : kOOB;
+  for (int q = 0; q < QB; ++q) {
+    const int c = lane + 64 * q, h = col0 + c;
+    const bool v = c < CW && h < H;
+    sbv[q] = v ? a.scale[l + 1][h] : T(0);
+    bbv[q] = (v && last) ? a.bias[h] : T(0);
+    offB[q] = v ? (uint32_t)c * ES : kOOB;
   }
   const uint32_t offG0 = (first && lane < K) ? (uint32_t)lane * ES : kOOB;
-  T cs0_b = 0, cs0_s = 0, csb_b[NTJ], csb_s[NTJ];
+  T cs0_b = 0, cs0_s = 0, csb_b[QB], csb_s[QB];
 #pragma unroll
-  for (int q = 0; q < NTJ; ++q) csb_b[q] = csb_s[q] = T(0);
+  for (int q = 0; q < QB; ++q) csb_b[q] = csb_s[q] = T(0);
   typename MF::acc_t acc[NTI][NTJ];
 #pragma unroll
   for (int ti = 0; ti < NTI; ++ti)
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
   // ends at the chunk's last row, so rows past it read 0; masked columns carry
   // kOOB offsets (kOOB + a row offset < 2^32 stays out of range).  Every load is
   // unconditional: a select on a load result would force its wait right there.
-  auto issue = [&](int64_t r0, PgStage<T, SR, NTJ>& st) {
+  auto issue = [&](int64_t r0, PgStage<T, SR, QB>& st) {
     const int64_t nr = r_end - r0;  // >= 1
     const auto rA = make_rsrc(srcA + r0 * ldA, (uint32_t)(((nr - 1) * ldA + K) * ES));
     const auto rG = make_rsrc(gA + r0 * a.gtot, (uint32_t)(((nr - 1) * a.gtot + K) * ES));
@@ -150,17 +152,18 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
     for (int m = 0; m < SR / 4; ++m) {
       const uint32_t rl = (uint32_t)(wave + 4 * m);
 #pragma unroll
-      for (int q = 0; q < kPgQ; ++q) st.a[m][q] = buf_load_elem<T>(rA, offA[q] + rl * (uint32_t)ldA * ES);
+      for (int q = 0; q < kPgQ; ++q)
+        if (64 * q < kpad) st.a[m][q] = buf_load_elem<T>(rA, offA[q] + rl * (uint32_t)ldA * ES);
       st.g0[m] = buf_load_elem<T>(rG, offG0 + rl * (uint32_t)a.gtot * ES);
 #pragma unroll
-      for (int q = 0; q < NTJ; ++q) {
+      for (int q = 0; q < QB; ++q) {
         st.gb[m][q] = buf_load_elem<T>(rB, offB[q] + rl * (uint32_t)a.gtot * ES);
         st.zb[m][q] = buf_load_elem<T>(rZ, offB[q] + rl * (uint32_t)a.ztot * ES);
       }
     }
   };
 
-  PgStage<T, SR, NTJ> st;
+  PgStage<T, SR, QB> st;
   issue(r_begin, st);
   for (int64_t r0 = r_begin; r0 < r_end; r0 += SR) {
     __syncthreads();  // the previous sub-chunk's MFMA reads are done
@@ -179,9 +182,9 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
       cs0_b += st.g0[m];  // G_0 reads 0 unless layer 0 / group 0
       cs0_s += st.g0[m] * st.a[m][0];
 #pragma unroll
-      for (int q = 0; q < NTJ; ++q) {
+      for (int q = 0; q < QB; ++q) {
         const T gv = st.gb[m][q];
-        sB[rl * LDB + lane + 64 * q] = gv * sbv[q];
+        if (lane + 64 * q < CW) sB[rl * LDB + lane + 64 * q] = gv * sbv[q];
         csb_b[q] += gv;
         csb_s[q] += gv * (st.zb[m][q] + bbv[q]);  // bbv = 0 unless the output layer
       }
@@ -189,15 +192,13 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
     __syncthreads();
     if (r0 + SR < r_end) issue(r0 + SR, st);  // in flight during the MFMA phase
     const int kk = lane >> 4, ii = lane & 15;
-    // Branch-free: B column tiles past H hold zeros (their products are dropped
-    // at the store), so every wave runs the same NTI x NTJ MFMAs per k-step.
 #pragma unroll
     for (int ks = 0; ks < SR / 4; ++ks) {
       T bf[NTJ], af[NTI];
 #pragma unroll
-      for (int jj = 0; jj < NTJ; ++jj) bf[jj] = sB[(4 * ks + kk) * LDB + (wave + 4 * jj) * 16 + ii];
+      for (int jj = 0; jj < NTJ; ++jj) bf[jj] = sB[(4 * ks + kk) * LDB + (wj + WJ * jj) * 16 + ii];
 #pragma unroll
-      for (int ti = 0; ti < NTI; ++ti) af[ti] = sA[(4 * ks + kk) * LDA + ti * 16 + ii];
+      for (int ti = 0; ti < NTI; ++ti) af[ti] = sA[(4 * ks + kk) * LDA + (wi + WI * ti) * 16 + ii];
 #pragma unroll
       for (int ti = 0; ti < NTI; ++ti)
 #pragma unroll
@@ -211,23 +212,24 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
   for (int ti = 0; ti < NTI; ++ti) {
 #pragma unroll
     for (int jj = 0; jj < NTJ; ++jj) {
-      const int h = col0 + (wave + 4 * jj) * 16 + (lane & 15);
+      const int h = col0 + (wj + WJ * jj) * 16 + (lane & 15);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const int k = ti * 16 + MF::row(lane, v);
+        const int k = (wi + WI * ti) * 16 + MF::row(lane, v);
         if (k < K && h < H) part[a.off_W[l] + (int64_t)k * H + h] = acc[ti][jj][v];
       }
     }
   }
   // ---- BN column sums: combine the 4 wavefronts (row phases) through LDS ----
   __syncthreads();  // LDS reuse
-  T* red = sA;  // [4 waves][2][CW] (B side), then [4 waves][2][64] (BN_0)
+  T* red = sA;  // [4 waves][2][64*QB] (B side), then [4 waves][2][64] (BN_0)
+  constexpr int RW = 64 * QB;
 #pragma unroll
-  for (int q = 0; q < NTJ; ++q) {
-    red[(wave * 2 + 0) * CW + lane + 64 * q] = csb_b[q];
-    red[(wave * 2 + 1) * CW + lane + 64 * q] = csb_s[q];
+  for (int q = 0; q < QB; ++q) {
+    red[(wave * 2 + 0) * RW + lane + 64 * q] = csb_b[q];
+    red[(wave * 2 + 1) * RW + lane + 64 * q] = csb_s[q];
   }
-  T* red0 = sA + 8 * CW;
+  T* red0 = sA + 8 * RW;
   red0[(wave * 2 + 0) * 64 + lane] = cs0_b;
   red0[(wave * 2 + 1) * 64 + lane] = cs0_s;
   __syncthreads();
@@ -235,8 +237,8 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
     T sb = 0, ss = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      sb += red[(w * 2 + 0) * CW + tid];
-      ss += red[(w * 2 + 1) * CW + tid];
+      sb += red[(w * 2 + 0) * RW + tid];
+      ss += red[(w * 2 + 1) * RW + tid];
     }
     part[a.off_beta[l + 1] + col0 + tid] = sb;
     part[a.off_gamma[l + 1] + col0 + tid] = ss;
@@ -263,8 +265,17 @@ __global__ __launch_bounds__(256) void k_param_grads_reduce(const PgArgs<T> a, i
   if (p >= a.ptot + Hout) return;
   const bool is_b = p >= a.ptot;
   const int64_t src = is_b ? a.off_beta[L + 1] + (p - a.ptot) : p;
+  const T* col = a.part + src;
   T s = 0;
-  for (int c = 0; c < nchunks; ++c) s += a.part[(int64_t)c * a.ptot + src];
+  int c = 0;
+  for (; c + 8 <= nchunks; c += 8) {  // 8 loads in flight, summed in chunk order
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = col[(int64_t)(c + u) * a.ptot];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; c < nchunks; ++c) s += col[(int64_t)c * a.ptot];
   if (is_b) {
     s = a.scale[L + 1][p - a.ptot] * s;
   } else if (p < a.off_beta[0]) {  // gamma block comes first

@@ -24,9 +24,12 @@ constexpr int kMrPrefetch = 8;
 
 template <typename T>
 struct MrCfg;
+#ifndef DPAC_MR_RT_F32
+#define DPAC_MR_RT_F32 1
+#endif
 template <>
 struct MrCfg<float> {
-  static constexpr int RT = 4;  // 64 rows per workgroup
+  static constexpr int RT = DPAC_MR_RT_F32;  // 16 rows per workgroup: occupancy beats B reuse (measured)
 };
 template <>
 struct MrCfg<double> {

