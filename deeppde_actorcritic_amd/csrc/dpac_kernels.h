@@ -103,6 +103,7 @@ constexpr int ring_kb(int frame_bytes, int budget_vgprs, int cap) {
 #define DPAC_ABLATE 0
 #endif
 
+
 // sqrt: the hardware v_sqrt_f32 for float (1 ulp), correctly rounded for double.
 __device__ __forceinline__ float dsqrt(float v) { return __builtin_amdgcn_sqrtf(v); }
 __device__ __forceinline__ double dsqrt(double v) { return sqrt(v); }
@@ -748,6 +749,7 @@ __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, i
 }
 
 #include "dpac_rollout_nn.h"
+#include "dpac_rollout_nn4.h"
 
 // ---------------------------------------------------------------------------
 // Launcher for one (T, equation functor, D).
@@ -770,6 +772,15 @@ NnMlp<T> nn_mlp(const dpac_mlp& h) {
   for (int i = 0; i <= m.L; ++i) m.weight[i] = (const T*)h.weight[i];
   m.bias = (const T*)h.bias;
   return m;
+}
+
+// Row tile of the fused NN rollout for float: 4 (4x4x1 MFMA blocks) or 16
+// (16x16x4 tiles; float64 always uses these); by default 4 for B <= 1024.
+// DPAC_NN_TILE=4 / 16 forces one (tests compare the two).
+inline int nn_tile_rows() {
+  const char* e = getenv("DPAC_NN_TILE");  // read per launch: tests switch it in-process
+  const int v = e ? atoi(e) : 0;
+  return (v == 4 || v == 16) ? v : 0;     // 0: by batch size
 }
 
 inline dim3 grid_for(int64_t B, int P) {
@@ -909,8 +920,30 @@ int run_op(const OpArgs& a) {
       r.x = (T*)a.x_out; r.dt = (T*)a.dt; r.coef = (T*)a.coef; r.u = (T*)a.u_out;
       r.y = (T*)a.y; r.disc = (T*)a.disc;
       r.save_z = (T*)a.save_z; r.save_disc = (T*)a.save_disc; r.save_flag = a.save_flag;
-      const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
       const bool cost = a.y != nullptr;
+      if constexpr (std::is_same<T, float>::value) {
+        // 4-row MFMA blocks (dpac_rollout_nn4.h) where the 16-row tiles would leave
+        // most CUs idle: 4x4x1 costs 4x the cycles per flop of 16x16x4, and measured
+        // 11.4 vs 15.4 us per step at B <= 1024, 15.8 vs 15.4 at 2048, 31 vs 15.4 at 4096
+        const int tile = nn_tile_rows();
+        if (tile == 4 || (tile == 0 && a.B <= 1024)) {
+          const int rg = a.B <= 1024 ? 1 : 2;
+          const dim3 g4((unsigned)((a.B + 4 * rg - 1) / (4 * rg))), b4(kN4Threads);
+#define DPAC_ROLL_NN4(SCH, CO, RG) \
+  hipLaunchKernelGGL((k_rollout_nn4<T, E, D, SCH, CO, RG>), g4, b4, 0, s, eq, c, m, r)
+#define DPAC_ROLL_NN4_RG(SCH, CO) \
+  if (rg == 1) { DPAC_ROLL_NN4(SCH, CO, 1); } else { DPAC_ROLL_NN4(SCH, CO, 2); }
+          if (adaptive) {
+            if (cost) { DPAC_ROLL_NN4_RG(DPAC_SCHEME_ADAPTIVE, true) } else { DPAC_ROLL_NN4_RG(DPAC_SCHEME_ADAPTIVE, false) }
+          } else {
+            if (cost) { DPAC_ROLL_NN4_RG(DPAC_SCHEME_NAIVE, true) } else { DPAC_ROLL_NN4_RG(DPAC_SCHEME_NAIVE, false) }
+          }
+#undef DPAC_ROLL_NN4_RG
+#undef DPAC_ROLL_NN4
+          break;
+        }
+      }
+      const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
 #define DPAC_ROLL_NN(SCH, CO) \
   hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1>), ngrid, nblock, 0, s, eq, c, m, r)
       if (adaptive) {

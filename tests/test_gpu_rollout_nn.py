@@ -237,3 +237,33 @@ def test_fused_bptt_fp32_ekn():
         ops.BPTT_MODE = "fused"
     for a, b in zip(grads["fused"], grads["loop"]):
         assert rel_close(a.cpu(), b.cpu(), 1e-4)
+
+
+@pytest.mark.parametrize("name,d,hidden,B", [("LQR", 20, (200, 200, 200), 2048), ("EKN", 20, (64, 64, 64), 37),
+                                             ("VDP", 10, (48, 130, 33), 1500), ("LQR_var", 5, (256, 256, 256, 256), 5),
+                                             ("LQR", 5, (4, 200), 1030)])
+def test_fp32_four_row_kernel_matches_sixteen_row(name, d, hidden, B, monkeypatch):
+    """The float rollout on 4x4x1 MFMA blocks (dpac_rollout_nn4.h, default for B <= 1024) against the
+    16x16x4 kernel (DPAC_NN_TILE=16) on identical inputs: only the order of the K sums
+    differs, so <= 1% of trajectories may flip an exit decision and matched ones agree to
+    2e-4 (1+|b|); both RG = 1 (B <= 1024) and RG = 2 workgroups and partial ones."""
+    N, T = 30, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme="adaptive", dtype="float32")
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, _ = actor_pair(cfg, torch.float32)
+    eqp = ep.params()
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=17, dtype=torch.float32, device=DEV)
+    out = {}
+    for tile in ("4", "16"):
+        monkeypatch.setenv("DPAC_NN_TILE", tile)
+        out[tile] = ops.rollout_nn(eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, net.mlp_view(),
+                                   cost_order=_lib.COST_ACTOR, save=True)
+    xa, dta, ca, ua, ya, da, sa = out["4"]
+    xb, dtb, cb, ub, yb, db, sb = out["16"]
+    same = torch.all(ca == cb, dim=1).cpu().numpy()
+    assert np.mean(~same) <= 1e-2
+    assert rel_close(xa[:, same].cpu(), xb[:, same].cpu(), 2e-4)
+    assert rel_close(ua[:, same].cpu(), ub[:, same].cpu(), 2e-4)
+    assert rel_close(ya[same].cpu(), yb[same].cpu(), 2e-4)
+    assert rel_close(sa[0][:, same].cpu(), sb[0][:, same].cpu(), 2e-4)  # saved z
+    assert torch.equal(sa[1][:, same], sb[1][:, same])                  # saved flags
