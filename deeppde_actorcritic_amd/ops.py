@@ -200,39 +200,59 @@ class _ActorRolloutNN(torch.autograd.Function):
     def backward(ctx, g_y, g_disc, g_xN):
         x, u, dw, z, flag, disc_t, rs, *params = ctx.saved_tensors
         eqp, scheme, T, N, ekn, L = ctx.cfg
-        gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
-        B, d = x.shape[1], x.shape[2]
-        widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
-        s = [rs * g for g in gam]
-        zoff = np.cumsum([0] + widths[1:]).tolist()
-        zl = [None] + [z[:, :, zoff[i - 1]:zoff[i]] for i in range(1, L + 2)]
-        gx_in = None if g_xN is None else g_xN.contiguous()
-        gd_in = None if g_disc is None else g_disc.contiguous()
-        gy_in = None if g_y is None else g_y.contiguous()
-        if BPTT_MODE == "fused":
-            G = _bptt_fused(eqp, scheme, T, N, ekn, L, x, u, dw, z, flag, disc_t, s, bet, Ws, b,
-                            widths, gx_in, gd_in, gy_in)
-        else:
-            G = _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b,
-                           widths, gx_in, gd_in, gy_in)
-        if PARAM_GRADS == "kernel":
-            grads = mlp_param_grads(MlpView(s, bet, Ws, b, ekn), x[:N].reshape(N * B, d),
-                                    z.reshape(N * B, -1), G_all(G).reshape(N * B, -1), params)
-            return (None,) * 8 + tuple(grads)
-        # parameter gradients over all N*B rows (PyTorch reference path)
-        rows = lambda tt: tt.reshape(N * B, -1)
-        zin = [x[:N]] + [zl[i] for i in range(1, L + 1)] + [zl[L + 1] + b]
-        dgam = [rs * torch.sum(rows(G[i] * zin[i]), 0) for i in range(L + 2)]
-        dbet = [torch.sum(rows(G[i]), 0) for i in range(L + 2)]
-        A = [torch.addcmul(bet[0], x[:N], s[0])]
-        for i in range(1, L + 1):
-            yl = torch.addcmul(bet[i], zl[i], s[i])
-            A.append(yl + torch.relu(yl))
-        # per-step partial products summed over N (split-K; one GEMM with an N*B-long
-        # reduction runs far below the MFMA rate)
-        dW = [torch.bmm(A[i].transpose(1, 2), G[i + 1] * s[i + 1]).sum(0) for i in range(L + 1)]
-        db = torch.sum(rows(G[L + 1] * s[L + 1]), 0)
-        return (None, None, None, None, None, None, None, None, *dgam, *dbet, *dW, db)
+        grads = actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, (x, u, dw, z, flag, disc_t),
+                                 g_y, g_disc, g_xN)
+        return (None,) * 8 + tuple(grads)
+
+
+def actor_rollout_saves(eqp, scheme: int, x0, dw, total_time: float, num_steps: int, net):
+    """The actor's rollout with `net` as control and the backward saves, no autograd:
+    (y [B], disc_N [B], x_N [B, d], saved) with saved = (x, u, dw, z, flag, disc_t) as
+    actor_bptt_grads takes it (the forward of _ActorRolloutNN)."""
+    x, dt, coef, u, y, disc, (z, flag, disc_t) = rollout_nn(
+        eqp, scheme, x0, dw, total_time, num_steps, net.mlp_view(), cost_order=_lib.COST_ACTOR,
+        save=True)
+    return y, disc, x[num_steps], (x, u, dw.contiguous(), z, flag, disc_t)
+
+
+def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_xN):
+    """Gradients of DeepNN.trainable_variables() (params) of the actor from the saves of
+    its fused rollout and the upstream gradients of (y, disc_N, x_N), each optional:
+    the BPTT of solver.py:92-97 (dpac_rollout_nn_bwd, then dpac_mlp_param_grads)."""
+    x, u, dw, z, flag, disc_t = saved
+    L = (len(params) - 1) // 3 - 1
+    gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
+    B, d = x.shape[1], x.shape[2]
+    widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+    s = [rs * g for g in gam]
+    zoff = np.cumsum([0] + widths[1:]).tolist()
+    zl = [None] + [z[:, :, zoff[i - 1]:zoff[i]] for i in range(1, L + 2)]
+    gx_in = None if g_xN is None else g_xN.contiguous()
+    gd_in = None if g_disc is None else g_disc.contiguous()
+    gy_in = None if g_y is None else g_y.contiguous()
+    if BPTT_MODE == "fused":
+        G = _bptt_fused(eqp, scheme, T, N, ekn, L, x, u, dw, z, flag, disc_t, s, bet, Ws, b,
+                        widths, gx_in, gd_in, gy_in)
+    else:
+        G = _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b,
+                       widths, gx_in, gd_in, gy_in)
+    if PARAM_GRADS == "kernel":
+        return mlp_param_grads(MlpView(s, bet, Ws, b, ekn), x[:N].reshape(N * B, d),
+                               z.reshape(N * B, -1), G_all(G).reshape(N * B, -1), params)
+    # parameter gradients over all N*B rows (PyTorch reference path)
+    rows = lambda tt: tt.reshape(N * B, -1)
+    zin = [x[:N]] + [zl[i] for i in range(1, L + 1)] + [zl[L + 1] + b]
+    dgam = [rs * torch.sum(rows(G[i] * zin[i]), 0) for i in range(L + 2)]
+    dbet = [torch.sum(rows(G[i]), 0) for i in range(L + 2)]
+    A = [torch.addcmul(bet[0], x[:N], s[0])]
+    for i in range(1, L + 1):
+        yl = torch.addcmul(bet[i], zl[i], s[i])
+        A.append(yl + torch.relu(yl))
+    # per-step partial products summed over N (split-K; one GEMM with an N*B-long
+    # reduction runs far below the MFMA rate)
+    dW = [torch.bmm(A[i].transpose(1, 2), G[i + 1] * s[i + 1]).sum(0) for i in range(L + 1)]
+    db = torch.sum(rows(G[L + 1] * s[L + 1]), 0)
+    return [*dgam, *dbet, *dW, db]
 
 
 # "fused": the reverse time loop as one dpac_rollout_nn_bwd launch; "loop": the
@@ -255,11 +275,13 @@ _WS_CACHE = {}
 
 
 def _workspace(nbytes: int, device) -> torch.Tensor:
-    """A reusable device scratch buffer (one per device, grown on demand; the
-    stream order of its users makes sharing safe)."""
-    key = (device.type, device.index)
+    """A reusable device scratch buffer, one per (device, size) and never freed: a
+    captured HIP graph keeps the address it saw, so a buffer must outlive every graph
+    that used it.  Its users run stream-ordered (the overlapped actor forward uses
+    none), which makes sharing safe."""
+    key = (device.type, device.index, int(nbytes))
     ws = _WS_CACHE.get(key)
-    if ws is None or ws.numel() < nbytes:
+    if ws is None:
         ws = _WS_CACHE[key] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
     return ws
 
@@ -428,14 +450,19 @@ class _RowMLP(torch.autograd.Function):
         return (g_x, None, *grads)
 
 
-def row_mlp(net, x: torch.Tensor) -> torch.Tensor:
-    """net(x) before the Eikonal head, x [..., d] -> [..., w_out], through the kernels."""
+def row_mlp(net, x: torch.Tensor, const_params: bool = False) -> torch.Tensor:
+    """net(x) before the Eikonal head, x [..., d] -> [..., w_out], through the kernels.
+    const_params: the parameters are constants for autograd (only dL/dx is formed),
+    as for the critic's V inside the actor's tape (solver.py:95 watches the actor)."""
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     if x2.stride(1) != 1:
         x2 = x2.contiguous()
-    if torch.is_grad_enabled() and (x2.requires_grad or any(p.requires_grad for p in net.trainable_variables())):
-        out = _RowMLP.apply(x2, net.bn_rs, *net.trainable_variables())
+    params = net.trainable_variables()
+    if const_params:
+        params = [p.detach() for p in params]
+    if torch.is_grad_enabled() and (x2.requires_grad or any(p.requires_grad for p in params)):
+        out = _RowMLP.apply(x2, net.bn_rs, *params)
     else:
         out, _ = mlp_rows(net.mlp_view(), x2)
     return out.reshape(*lead, out.shape[-1])

@@ -77,13 +77,14 @@ class DeepNN(nn.Module):
         self.register_buffer("bn_rs", torch.rsqrt(torch.tensor(1.0 + BN_EPS, dtype=dtype)).to(device),
                              persistent=False)
 
-    def forward(self, x, training=False, need_grad=False):
+    def forward(self, x, training=False, need_grad=False, const_params=False):
         """x [rows, d], or [S, R, d] for a stack of S batches (e.g. the critic's G over
         all N steps): then every product is a batched GEMM over S with the weight
         broadcast, so autograd forms the weight gradients as S partial products and
-        a sum instead of one GEMM with a 10^5-long reduction."""
+        a sum instead of one GEMM with a 10^5-long reduction.  const_params: the
+        parameters are not differentiated (kernel path: no parameter-gradient work)."""
         if x.is_cuda and ops.ROW_MLP == "kernel" and self.fused_ok():
-            y = ops.row_mlp(self, x)  # hand-written MFMA kernels (dpac_mlp_rows_*)
+            y = ops.row_mlp(self, x, const_params)  # hand-written MFMA kernels (dpac_mlp_rows_*)
             return self._ekn(y) if self.ekn_head else y
         rs = self.bn_rs
         g, bt, W = self.bn_gamma, self.bn_beta, self.W
@@ -206,7 +207,9 @@ class ActorModel(nn.Module):
         if cheat_value:
             term = ops.v_true(eqp, xN)
         else:
-            term = model_critic.NN_value(xN, training)[:, 0]
+            # the actor's tape watches only the actor (solver.py:95): V's parameters
+            # are constants here
+            term = model_critic.NN_value(xN, training, const_params=True)[:, 0]
         return (y + term * disc).unsqueeze(1)  # solver.py:220-223
 
 
@@ -289,6 +292,42 @@ class _GradGraph:
         return list(self.out)
 
 
+class _SplitActorGraphs:
+    """The actor step as two HIP graphs: the fused forward rollout with its backward
+    saves (replayed on a side stream, so it runs beside the critic step: it reads only
+    the actor's parameters, which the critic step does not change) and the gradient
+    from those saves (after the critic update, which the terminal value V(x_N) needs;
+    solver.py:67-70 order).  The backward graph reads the forward graph's outputs in
+    place: nothing is copied between them."""
+
+    def __init__(self, fwd_fn, bwd_fn, batch: TrajectoryBatch, side):
+        self.static = TrajectoryBatch(*[t.clone() for t in batch])
+        self.side = side
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up outside the capture (allocator, autograd)
+            for _ in range(2):
+                bwd_fn(fwd_fn(self.static))
+        torch.cuda.current_stream().wait_stream(side)
+        self.g_fwd, self.g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fwd):
+            self.fwd = fwd_fn(self.static)
+        with torch.cuda.graph(self.g_bwd):
+            self.out = bwd_fn(self.fwd)
+
+    def launch_forward(self, batch: TrajectoryBatch):
+        """On the side stream, after the work queued so far on the current stream."""
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            for dst, src in zip(self.static, batch):
+                dst.copy_(src)
+            self.g_fwd.replay()
+
+    def grads(self):
+        torch.cuda.current_stream().wait_stream(self.side)
+        self.g_bwd.replay()
+        return list(self.out)
+
+
 def _huber_mean(delta):
     """solver.py:76-77 (quadratic inside |delta| < 50, linear outside)."""
     a = torch.abs(delta)
@@ -357,6 +396,7 @@ class ActorCriticSolver(object):
         self._calls = 0
         self.hip_graphs = (self.sampler == "device") if graphs is None else bool(graphs)
         self._graphs = {}
+        self._side = None
         if self.sampler == "host":
             self._np_rng_state = None
 
@@ -419,6 +459,65 @@ class ActorCriticSolver(object):
         cnt = train_data[0].shape[0]
         g = self.par.allreduce_grads(g, cnt, total or cnt * self.par.world)
         self.optimizer_critic.apply_gradients(zip(g, self.critic_variables()))
+
+    # ---- the actor step split around the critic step (overlap) ---------------
+    def _actor_split_ok(self):
+        return (self.hip_graphs and self.train_config.train == "actor-critic"
+                and self.model_actor.NN_control.fused_ok() and ops.BPTT_MODE == "fused")
+
+    def actor_forward(self, data):
+        """The actor's rollout with saves (solver.py:207-219 forward), no autograd."""
+        ma, ec = self.model_actor, self.eqn_config
+        d = Equation.to_native(data, self.dtype)
+        return ops.actor_rollout_saves(self.bsde.params(), ma.scheme, d.x0, d.dw, ec.total_time_actor,
+                                       ec.num_time_interval_actor, ma.NN_control)
+
+    def actor_grads_from(self, fwd):
+        """grad_actor from actor_forward's outputs: loss = mean(y + V(x_N)*disc_N)
+        (solver.py:80-83, 220-223) differentiated by hand at (y, disc_N, x_N), then the
+        BPTT kernels; V's parameters are constants (the tape watches the actor)."""
+        y, disc, xN, saved = fwd
+        B = y.shape[0]
+        eqp = self.bsde.params()
+        if self.cheat_value_in_actor:
+            term = ops.equation_eval(eqp, _lib.EVAL_V_TRUE, xN)
+            gV = ops.equation_eval(eqp, _lib.EVAL_V_GRAD, xN)
+        else:
+            xl = xN.detach().requires_grad_(True)
+            with torch.enable_grad():
+                v = self.model_critic.NN_value(xl, False, const_params=True)[:, 0]
+                gV, = torch.autograd.grad(v.sum(), xl)
+            term = v.detach()
+        g_y = torch.full_like(y, 1.0 / B)
+        g_disc = term / B
+        g_xN = gV * (disc / B).unsqueeze(1)
+        net = self.model_actor.NN_control
+        ec = self.eqn_config
+        return ops.actor_bptt_grads(eqp, self.model_actor.scheme, ec.total_time_actor,
+                                    ec.num_time_interval_actor, net.ekn_head, net.bn_rs,
+                                    net.trainable_variables(), saved, g_y, g_disc, g_xN)
+
+    def train_iteration(self, data_critic, data_actor, total=None):
+        """One iteration of solver.py:67-70 (critic step, then actor step).  With HIP
+        graphs the actor's forward rollout runs on a side stream during the critic step."""
+        if not self._actor_split_ok():
+            self.train_step_critic(data_critic, total)
+            self.train_step_actor(data_actor, total)
+            return
+        da = Equation.to_native(data_actor, self.dtype)
+        key = ("actor_split", tuple(da.dw.shape))
+        sg = self._graphs.get(key)
+        if sg is None:
+            if self._side is None:
+                self._side = torch.cuda.Stream()
+            sg = self._graphs[key] = _SplitActorGraphs(self.actor_forward, self.actor_grads_from,
+                                                       da, self._side)
+        sg.launch_forward(da)
+        self.train_step_critic(data_critic, total)
+        g = sg.grads()
+        cnt = da.x0.shape[0]
+        g = self.par.allreduce_grads(g, cnt, total or cnt * self.par.world)
+        self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))
 
     def train_step_actor(self, train_data, total=None):
         g = self._grads("actor", lambda d: self.grad_actor(
@@ -523,8 +622,13 @@ class ActorCriticSolver(object):
                 if self.par.rank == 0:
                     print("true loss actor: ", true_loss_actor)
                 training_history.append([0, 0.0, true_loss_actor, 0.0, 0.0, 0.0, 0.0, 0.0, elapsed_time])
-            if self.train_config.train in ("actor-critic", "critic"):
+            if self.train_config.train == "actor-critic":
+                # both samples first, in the reference's order (critic, then actor)
+                dc = self.sample(nc.batch_size, ec.num_time_interval_critic)
+                da = self.sample(nc.batch_size, ec.num_time_interval_actor)
+                self.train_iteration(dc, da, nc.batch_size)
+            elif self.train_config.train == "critic":
                 self.train_step_critic(self.sample(nc.batch_size, ec.num_time_interval_critic), nc.batch_size)
-            if self.train_config.train in ("actor-critic", "actor"):
+            else:
                 self.train_step_actor(self.sample(nc.batch_size, ec.num_time_interval_actor), nc.batch_size)
         return np.array(training_history), x0, y, true_y, z, true_z, grad_y

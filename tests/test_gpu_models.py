@@ -129,3 +129,40 @@ def test_hip_graph_steps_match_eager(name, d, td):
         res.append([v.detach().cpu() for v in sp.critic_variables() + sp.actor_variables()])
     for a, b in zip(*res):
         assert rel_close(a, b, 1e-12)
+
+
+@pytest.mark.parametrize("name,d,td,train,cheat", [("LQR", 20, "TD1", "actor-critic", False),
+                                                  ("EKN", 5, "TD2", "actor-critic", False),
+                                                  ("VDP", 4, "TD1", "actor-critic", False)])
+def test_overlapped_iteration_matches_sequential(name, d, td, train, cheat):
+    """train_iteration (the actor's forward rollout on a side stream during the critic
+    step, its gradient from the saves afterwards) gives the parameters of sequential
+    eager critic + actor steps (float64, 1e-12)."""
+    cfg = full_config(name, d, N=10, hidden=(32, 32), batch=64, valid=64, td=td, train=train)
+    res = []
+    for overlap in (False, True):
+        bp = getattr(peq, name)(cfg.eqn_config)
+        sp = psol.ActorCriticSolver(cfg, bp, seed=7, sampler="device", graphs=overlap)
+        for _ in range(3):
+            dc = sp.sample(64, 10)
+            da = sp.sample(64, 10)
+            if overlap:
+                sp.train_iteration(dc, da)
+            else:
+                sp.train_step_critic(dc)
+                sp.train_step_actor(da)
+        res.append([v.detach().cpu() for v in sp.critic_variables() + sp.actor_variables()])
+    for a, b in zip(*res):
+        assert rel_close(a, b, 1e-12)
+
+
+def test_actor_grads_from_saves_match_tape():
+    """actor_grads_from(actor_forward(batch)) equals grad_actor (autograd through the fused
+    rollout) on the same batch, float64."""
+    cfg = full_config("LQR", 20, N=12, hidden=(40, 40), batch=50, valid=50)
+    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=3, sampler="device", graphs=False)
+    data = sp.sample(50, 12)
+    g_tape = sp.grad_actor(data, False, False, False)
+    g_split = sp.actor_grads_from(sp.actor_forward(data))
+    for a, b in zip(g_split, g_tape):
+        assert rel_close(a.cpu(), b.cpu(), 1e-12)
