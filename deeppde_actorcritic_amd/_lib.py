@@ -98,6 +98,9 @@ SIGNATURES = {
     "dpac_mlp_param_grads_workspace": [_I32, _I64, ctypes.POINTER(Mlp)],
     "dpac_mlp_param_grads": [_I32, _I64, ctypes.POINTER(Mlp), _D, _P, _I64, _P, _P, _P, _I64, _P,
                              _P],
+    "dpac_adam_apply": [_I32, _I32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_void_p),
+                        ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                        ctypes.POINTER(ctypes.c_void_p), _D, _D, _D, _D, _P],
 }
 _RESTYPES = {"dpac_abi_version": ctypes.c_int32, "dpac_last_error": ctypes.c_char_p,
              "dpac_supported": ctypes.c_int32, "dpac_mlp_param_grads_workspace": ctypes.c_int64}

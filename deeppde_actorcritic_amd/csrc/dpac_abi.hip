@@ -28,6 +28,9 @@ int mlp_rows_fwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void
                         void* out, void* save_z, hipStream_t s);
 int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
                         const void* save_z, const void* g_out, void* G, void* g_x, hipStream_t s);
+int adam_launch(int dtype, int n, const int64_t* numel, void* const* var, const void* const* grad,
+                void* const* m, void* const* v, double alpha, double b1, double b2, double eps,
+                hipStream_t s);
 
 namespace {
 thread_local std::string g_err;
@@ -621,6 +624,28 @@ int dpac_equation_eval(const dpac_eqn_params* eq, int32_t what, int32_t dtype, i
   a.what = what; a.dtype = dtype; a.B = num_sample; a.N = 1; a.T = 1.0; a.x = x; a.u = u;
   a.out = out; a.stream = (hipStream_t)stream;
   return launch(a);
+}
+
+int dpac_adam_apply(int32_t dtype, int32_t n_tensors, const int64_t* numel, void* const* var,
+                    const void* const* grad, void* const* m, void* const* v, double alpha,
+                    double beta_1, double beta_2, double epsilon, void* stream) {
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
+  if (n_tensors < 0) return fail(DPAC_EINVAL, "n_tensors must be >= 0 (got %d)", n_tensors);
+  if (n_tensors == 0) return ok();
+  DPAC_REQUIRE(numel);
+  DPAC_REQUIRE(var);
+  DPAC_REQUIRE(grad);
+  DPAC_REQUIRE(m);
+  DPAC_REQUIRE(v);
+  for (int i = 0; i < n_tensors; ++i) {
+    if (numel[i] < 1) return fail(DPAC_EINVAL, "tensor %d: numel must be >= 1", i);
+    if (!var[i] || !grad[i] || !m[i] || !v[i])
+      return fail(DPAC_EINVAL, "tensor %d: a pointer is NULL", i);
+  }
+  const int r = adam_launch(dtype, n_tensors, numel, var, grad, m, v, alpha, beta_1, beta_2,
+                            epsilon, (hipStream_t)stream);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
 }
 
 }  // extern "C"

@@ -274,12 +274,13 @@ def G_all(G):
 _WS_CACHE = {}
 
 
-def _workspace(nbytes: int, device) -> torch.Tensor:
-    """A reusable device scratch buffer, one per (device, size) and never freed: a
+def _workspace(nbytes: int, device, tag: int = 0) -> torch.Tensor:
+    """A reusable device scratch buffer, one per (device, size, tag) and never freed: a
     captured HIP graph keeps the address it saw, so a buffer must outlive every graph
-    that used it.  Its users run stream-ordered (the overlapped actor forward uses
-    none), which makes sharing safe."""
-    key = (device.type, device.index, int(nbytes))
+    that used it.  Users of one tag run stream-ordered; work that runs beside them on
+    another stream (the critic's G-network backward beside the actor's BPTT) takes
+    its own tag."""
+    key = (device.type, device.index, int(nbytes), int(tag))
     ws = _WS_CACHE.get(key)
     if ws is None:
         ws = _WS_CACHE[key] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
@@ -292,18 +293,18 @@ def bn_rs_host(dtype) -> float:
     return float(torch.rsqrt(torch.tensor(1.0 + 1e-6, dtype=dtype)))
 
 
-def mlp_param_grads(view: "MlpView", x, z, G, like):
+def mlp_param_grads(view: "MlpView", x, z, G, like, ws_tag: int = 0):
     """Gradients of DeepNN's trainable variables (order of trainable_variables()) from
     the backward chain's G [R, Σ widths], the saved z [R, Σ widths[1:]] and the
     network input x [R, d]; one dpac_mlp_param_grads launch.  `like` gives the
-    parameter shapes."""
+    parameter shapes; ws_tag selects the scratch buffer (_workspace)."""
     _require_gpu(x, z, G)
     R = x.shape[0]
     dt = _dtype_id(x)
     nbytes = _lib.load().dpac_mlp_param_grads_workspace(dt, R, ctypes.byref(view.struct))
     if nbytes < 0:
         raise _lib.DpacError("dpac_mlp_param_grads_workspace", nbytes, _lib.load().dpac_last_error().decode())
-    ws = _workspace(int(nbytes), x.device)
+    ws = _workspace(int(nbytes), x.device, ws_tag)
     total = sum(p.numel() for p in like)
     flat = torch.empty(total, dtype=x.dtype, device=x.device)
     if x.stride(1) != 1 or not z.is_contiguous() or not G.is_contiguous():
@@ -433,21 +434,28 @@ class _RowMLP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_out):
         x, z, rs, *params = ctx.saved_tensors
-        L, gam, bet, Ws, b = _split_params(params)
-        s = [rs * g for g in gam]
-        view = MlpView(s, bet, Ws, b, False)
-        R = x.shape[0]
-        wt = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]
-        wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
-        G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
-        g_x = torch.empty(R, view.widths[0], dtype=x.dtype, device=x.device) \
-            if ctx.needs_input_grad[0] else None
-        call("dpac_mlp_rows_bwd", _dtype_id(x), R, ctypes.byref(view.struct), wt_ptrs, _ptr(z),
-             _ptr(g_out.contiguous()), _ptr(G), _ptr(g_x), _stream(x))
-        grads = [None] * len(params)
-        if any(ctx.needs_input_grad[2:]):
-            grads = mlp_param_grads(view, x, z, G, params)
-        return (g_x, None, *grads)
+        g_x, grads = row_mlp_backward(rs, params, x, z, g_out, ctx.needs_input_grad[0],
+                                      any(ctx.needs_input_grad[2:]))
+        return (g_x, None, *(grads if grads is not None else [None] * len(params)))
+
+
+def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, ws_tag: int = 0):
+    """The backward of mlp_rows(save=True) given dL/d(output) g_out [R, w_out]:
+    dpac_mlp_rows_bwd (the input-gradient chain: G of every BN output, and dL/dx if
+    want_x) then dpac_mlp_param_grads (if want_params).  params =
+    DeepNN.trainable_variables(); returns (g_x or None, parameter gradients or None)."""
+    L, gam, bet, Ws, b = _split_params(params)
+    s = [rs * g for g in gam]
+    view = MlpView(s, bet, Ws, b, False)
+    R = x.shape[0]
+    wt = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]
+    wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
+    G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
+    g_x = torch.empty(R, view.widths[0], dtype=x.dtype, device=x.device) if want_x else None
+    call("dpac_mlp_rows_bwd", _dtype_id(x), R, ctypes.byref(view.struct), wt_ptrs, _ptr(z),
+         _ptr(g_out.contiguous()), _ptr(G), _ptr(g_x), _stream(x))
+    grads = mlp_param_grads(view, x, z, G, params, ws_tag) if want_params else None
+    return g_x, grads
 
 
 def row_mlp(net, x: torch.Tensor, const_params: bool = False) -> torch.Tensor:
@@ -620,3 +628,34 @@ class _VTrue(torch.autograd.Function):
 
 def v_true(eqp, x):
     return _VTrue.apply(x, eqp)
+
+
+_ADAM_ARGS = {}
+
+
+def adam_apply(vs, gs, ms, ss, alpha: float, beta_1: float, beta_2: float, eps: float):
+    """One TF-form Adam step over parameter tensors vs with gradients gs and moments
+    ms, ss (all on the GPU, one dtype): one dpac_adam_apply launch on the current
+    stream.  The pointer arrays are cached per set of addresses (a replayed graph
+    hands back the same gradient buffers every step)."""
+    _require_gpu(*vs, *gs, *ms, *ss)
+    _check_same(vs[0], *vs, *gs, *ms, *ss)
+    key = tuple(t.data_ptr() for t in (*vs, *gs, *ms, *ss))
+    args = _ADAM_ARGS.get(key)
+    if args is None:
+        for group in (gs, ms, ss):
+            for v, t in zip(vs, group):
+                if t.shape != v.shape or not t.is_contiguous():
+                    raise ValueError("adam_apply: gradients and moments must match the "
+                                     "parameters' shapes and be contiguous")
+        if not all(v.is_contiguous() for v in vs):
+            raise ValueError("adam_apply: parameters must be contiguous")
+        n = len(vs)
+        arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+        args = (n, (ctypes.c_int64 * n)(*[v.numel() for v in vs]), arr(vs), arr(gs), arr(ms), arr(ss))
+        if len(_ADAM_ARGS) > 64:
+            _ADAM_ARGS.clear()
+        _ADAM_ARGS[key] = args
+    n, numel, pv, pg, pm, ps = args
+    call("dpac_adam_apply", _dtype_id(vs[0]), n, numel, pv, pg, pm, ps, float(alpha),
+         float(beta_1), float(beta_2), float(eps), _stream(vs[0]))

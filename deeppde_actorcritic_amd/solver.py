@@ -151,7 +151,9 @@ class CriticModel(nn.Module):
         self.scheme = self.train_config.scheme
         self.td = _lib.TD1 if self.train_config.TD_type == "TD1" else _lib.TD2
 
-    def forward(self, inputs, model_actor, training, cheat_control):
+    def forward(self, inputs, model_actor, training, cheat_control, G_fn=None):
+        """G_fn(x[:N]) -> G [N, B, d] replaces NN_value_grad when given (the split
+        critic step evaluates it with saves and makes it a leaf of the tape)."""
         x0, dw, x_bdry = Equation.to_native(inputs, self.NN_value.bn_rs.dtype)
         N = self.eqn_config.num_time_interval_critic
         T = self.eqn_config.total_time_critic
@@ -161,7 +163,8 @@ class CriticModel(nn.Module):
                                                model_actor.NN_control, cheat=cheat_control)
         G = None
         if self.td == _lib.TD1:
-            G = self.NN_value_grad(x[:N], training)  # [N, B, d], batched over the N steps
+            G = (G_fn(x[:N]) if G_fn is not None    # [N, B, d], batched over the N steps
+                 else self.NN_value_grad(x[:N], training))
         y, disc = ops.td_assemble(self.bsde.params(), self.td, x, u, dw, dt, coef, G,
                                   cost_order=_lib.COST_CRITIC)
         V = self.NN_value(torch.cat([x[0], x[N], x_bdry]), training)[:, 0]
@@ -242,7 +245,9 @@ class TFAdam:
         self.state = {}
 
     @torch.no_grad()
-    def apply_gradients(self, grads_and_vars):
+    def apply_gradients(self, grads_and_vars, advance=True):
+        """advance=False leaves `iterations` unchanged, so one optimizer step can be
+        applied in parts (disjoint variable sets, same lr and t)."""
         lr = self.schedule(self.iterations)
         t = self.iterations + 1
         alpha = lr * np.sqrt(1 - self.b2 ** t) / (1 - self.b1 ** t)
@@ -250,15 +255,21 @@ class TFAdam:
         for g, v in grads_and_vars:
             if g is None:
                 continue
-            m, s = self.state.setdefault(v, (torch.zeros_like(v), torch.zeros_like(v)))
-            gs.append(g); vs.append(v); ms.append(m); ss.append(s)
-        if gs:
+            st = self.state.get(v)
+            if st is None:
+                st = self.state[v] = (torch.zeros_like(v), torch.zeros_like(v))
+            gs.append(g); vs.append(v); ms.append(st[0]); ss.append(st[1])
+        if gs and gs[0].is_cuda:  # one dpac_adam_apply launch (same arithmetic, same order)
+            ops.adam_apply([v.data for v in vs], [g.detach().contiguous() for g in gs], ms, ss, alpha,
+                           self.b1, self.b2, self.eps)
+        elif gs:
             torch._foreach_add_(ms, torch._foreach_mul(torch._foreach_sub(gs, ms), 1 - self.b1))
             g2 = torch._foreach_mul(gs, gs)
             torch._foreach_add_(ss, torch._foreach_mul(torch._foreach_sub(g2, ss), 1 - self.b2))
             den = torch._foreach_add(torch._foreach_sqrt(ss), self.eps)
             torch._foreach_sub_(vs, torch._foreach_div(torch._foreach_mul(ms, alpha), den))
-        self.iterations += 1
+        if advance:
+            self.iterations += 1
 
     def state_dict(self):
         return {"iterations": self.iterations}
@@ -326,6 +337,43 @@ class _SplitActorGraphs:
         torch.cuda.current_stream().wait_stream(self.side)
         self.g_bwd.replay()
         return list(self.out)
+
+
+class _SplitCriticGraphs:
+    """The critic step as two HIP graphs, split at the G network's output: the front
+    (rollout, G forward with saves, TD assembly, V, the loss and its gradients for
+    V's variables and for G's output) and the G network's backward (input-gradient
+    chain + parameter gradients).  The back graph runs on a side stream beside the
+    actor's BPTT, which needs the updated V only (solver.py:221), not G."""
+
+    def __init__(self, front_fn, back_fn, batch: TrajectoryBatch, side):
+        self.static = TrajectoryBatch(*[t.clone() for t in batch])
+        self.side = side
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up outside the capture (allocator, autograd)
+            for _ in range(2):
+                back_fn(front_fn(self.static))
+        torch.cuda.current_stream().wait_stream(side)
+        self.g_front, self.g_back = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_front):
+            self.front_out = front_fn(self.static)
+        with torch.cuda.graph(self.g_back):
+            self.back_out = back_fn(self.front_out)
+
+    def front(self, batch: TrajectoryBatch):
+        """Gradients of V's variables (current stream)."""
+        for dst, src in zip(self.static, batch):
+            dst.copy_(src)
+        self.g_front.replay()
+        return list(self.front_out[0])
+
+    def launch_back(self, after: torch.cuda.Event):
+        """G's parameter gradients, replayed on the side stream once `after` (recorded
+        behind front()) has passed; use them on the side stream."""
+        self.side.wait_event(after)
+        with torch.cuda.stream(self.side):
+            self.g_back.replay()
+        return list(self.back_out)
 
 
 def _huber_mean(delta):
@@ -397,6 +445,7 @@ class ActorCriticSolver(object):
         self.hip_graphs = (self.sampler == "device") if graphs is None else bool(graphs)
         self._graphs = {}
         self._side = None
+        self._side_g = None
         if self.sampler == "host":
             self._np_rng_state = None
 
@@ -497,9 +546,51 @@ class ActorCriticSolver(object):
                                     ec.num_time_interval_actor, net.ekn_head, net.bn_rs,
                                     net.trainable_variables(), saved, g_y, g_disc, g_xN)
 
+    # ---- the critic step split at the G network (its backward beside the BPTT) ----
+    def _critic_split_ok(self):
+        mc = self.model_critic
+        return (self._actor_split_ok() and mc.td == _lib.TD1 and ops.ROW_MLP == "kernel"
+                and mc.NN_value_grad.fused_ok() and not mc.NN_value_grad.ekn_head)
+
+    def critic_front(self, data):
+        """grad_critic's loss (solver.py:73-78) with G = NN_value_grad(x_t) (solver.py:179)
+        evaluated once with saves and entering the tape as a leaf: returns (gradients
+        of V's variables, dL/dG [N*B, d], G's input rows, G's saves)."""
+        mc = self.model_critic
+        net = mc.NN_value_grad
+        held = {}
+
+        def G_fn(xs):
+            rows = xs.reshape(-1, xs.shape[-1])
+            with torch.no_grad():
+                out, z = ops.mlp_rows(net.mlp_view(), rows, save=True)
+            leaf = out.view(xs.shape[0], xs.shape[1], -1).requires_grad_(True)
+            held.update(rows=rows, z=z, leaf=leaf)
+            return leaf
+
+        d = Equation.to_native(data, self.dtype)
+        delta, delta_bdry = mc(d, self.model_actor, False, self.cheat_control_in_critic, G_fn=G_fn)
+        loss = (_huber_mean(delta) + _huber_mean(delta_bdry)) * 100
+        vs = mc.NN_value.trainable_variables()
+        g = torch.autograd.grad(loss, vs + [held["leaf"]], allow_unused=True)
+        gG = g[-1].reshape(held["rows"].shape[0], -1)
+        return list(g[:-1]), gG, held["rows"], held["z"]
+
+    def critic_G_back(self, front):
+        """G's parameter gradients from critic_front's outputs (dpac_mlp_rows_bwd +
+        dpac_mlp_param_grads, on their own scratch buffer: they run beside the BPTT)."""
+        _, gG, rows, z = front
+        net = self.model_critic.NN_value_grad
+        with torch.no_grad():
+            _, grads = ops.row_mlp_backward(net.bn_rs, net.trainable_variables(), rows, z, gG,
+                                            False, True, ws_tag=1)
+        return grads
+
     def train_iteration(self, data_critic, data_actor, total=None):
         """One iteration of solver.py:67-70 (critic step, then actor step).  With HIP
-        graphs the actor's forward rollout runs on a side stream during the critic step."""
+        graphs the actor's forward rollout runs on a side stream during the critic step;
+        under TD1 the critic's G-network backward and G's Adam update run on a second
+        side stream beside the actor's BPTT (which reads V, not G)."""
         if not self._actor_split_ok():
             self.train_step_critic(data_critic, total)
             self.train_step_actor(data_actor, total)
@@ -513,11 +604,39 @@ class ActorCriticSolver(object):
             sg = self._graphs[key] = _SplitActorGraphs(self.actor_forward, self.actor_grads_from,
                                                        da, self._side)
         sg.launch_forward(da)
-        self.train_step_critic(data_critic, total)
-        g = sg.grads()
+        if not self._critic_split_ok():
+            self.train_step_critic(data_critic, total)
+            cg = None
+        else:
+            dc = Equation.to_native(data_critic, self.dtype)
+            ckey = ("critic_split", tuple(dc.dw.shape))
+            cg = self._graphs.get(ckey)
+            if cg is None:
+                if self._side_g is None:
+                    self._side_g = torch.cuda.Stream()
+                cg = self._graphs[ckey] = _SplitCriticGraphs(self.critic_front, self.critic_G_back,
+                                                             dc, self._side_g)
+            ccnt = dc.x0.shape[0]
+            ctot = total or ccnt * self.par.world
+            gV = cg.front(dc)
+            front_done = torch.cuda.Event()
+            front_done.record()
+            gV = self.par.allreduce_grads(gV, ccnt, ctot)
+            # one Adam step of the critic in two parts: V now (the actor reads it), G beside the BPTT
+            self.optimizer_critic.apply_gradients(
+                zip(gV, self.model_critic.NN_value.trainable_variables()), advance=False)
+        g = sg.grads()  # the BPTT is queued before G's backward, so it claims its CUs first
+        if cg is not None:
+            gG = cg.launch_back(front_done)
+            with torch.cuda.stream(cg.side):
+                gG = self.par.allreduce_grads(gG, ccnt, ctot)
+                self.optimizer_critic.apply_gradients(
+                    zip(gG, self.model_critic.NN_value_grad.trainable_variables()))
         cnt = da.x0.shape[0]
         g = self.par.allreduce_grads(g, cnt, total or cnt * self.par.world)
         self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))
+        if cg is not None:
+            torch.cuda.current_stream().wait_stream(cg.side)
 
     def train_step_actor(self, train_data, total=None):
         g = self._grads("actor", lambda d: self.grad_actor(

@@ -310,6 +310,18 @@ int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, doubl
                          const void* x, int64_t ldx, const void* save_z, const void* G,
                          void* workspace, int64_t workspace_bytes, void* grads, void* stream);
 
+/* ---- optimizer step --------------------------------------------------
+ * One step of TF-form Adam (the reference's tf.keras Adam, solver.py:16-21;
+ * ResourceApplyAdam) over n_tensors parameter tensors of `dtype`, one launch:
+ *   m += (g - m)(1 - beta_1);  v += (g*g - v)(1 - beta_2);
+ *   var -= (m*alpha) / (sqrt(v) + epsilon),
+ * with alpha = lr*sqrt(1 - beta_2^t)/(1 - beta_1^t) formed by the caller.  Each
+ * operation rounds separately, in this order.  Arrays hold n_tensors device
+ * pointers / element counts; var, m, v are updated in place. */
+int dpac_adam_apply(int32_t dtype, int32_t n_tensors, const int64_t* numel, void* const* var,
+                    const void* const* grad, void* const* m, void* const* v, double alpha,
+                    double beta_1, double beta_2, double epsilon, void* stream);
+
 /* ---- device equation coefficients (for parity tests and metrics) -------
  * Evaluates one Equation method row-wise on x [B][d] (and u [B][c] where the
  * method takes a control): drift/sigma/w/Z/V_true/u_true/V_grad_true/b_tf

@@ -6,6 +6,7 @@ inside the actor's BPTT against the PyTorch product path.
 Tolerances: float64 |a-b| <= 1e-11 (1+|b|) (only the summation order differs);
 float32 vs the float64 reference: 2e-5 (1+|b|) relative to the largest entry.
 """
+import numpy as np
 import pytest
 import torch
 
@@ -219,3 +220,37 @@ def test_row_mlp_stacked_input_and_errors():
     assert lib.dpac_mlp_rows_fwd(_lib.F64, 10, ctypes.byref(view.struct),
                                  ctypes.c_void_p(x.data_ptr()), 3, ctypes.c_void_p(x.data_ptr()),
                                  None, None) == _lib.DPAC_EINVAL  # ldx < d
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_adam_kernel_matches_foreach_update(dtype):
+    """dpac_adam_apply (one launch over a list of tensors, more than one launch's 32)
+    gives bitwise the TF-form Adam update written as separate torch foreach ops on
+    the GPU (solver.TFAdam's previous path), over three steps.  (Torch's CPU sqrt and
+    division differ from the GPU's in the last bit, so the reference runs on the GPU.)"""
+    from deeppde_actorcritic_amd import ops
+    gen = torch.Generator().manual_seed(5)
+    shapes = [(200, 200), (200,), (20, 1), (1,), (20, 200)] * 7  # 35 tensors
+    vs = [torch.randn(s, generator=gen, dtype=dtype) for s in shapes]
+    ref = [v.cuda() for v in vs]
+    dev = [v.cuda() for v in vs]
+    m_ref = [torch.zeros_like(v) for v in ref]
+    s_ref = [torch.zeros_like(v) for v in ref]
+    m_dev = [torch.zeros_like(v) for v in dev]
+    s_dev = [torch.zeros_like(v) for v in dev]
+    b1, b2, eps = 0.9, 0.999, 1e-8
+    for t in range(1, 4):
+        gs = [torch.randn(s, generator=gen, dtype=dtype).cuda() for s in shapes]
+        alpha = 1e-3 * np.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+        torch._foreach_add_(m_ref, torch._foreach_mul(torch._foreach_sub(gs, m_ref), 1 - b1))
+        g2 = torch._foreach_mul(gs, gs)
+        torch._foreach_add_(s_ref, torch._foreach_mul(torch._foreach_sub(g2, s_ref), 1 - b2))
+        den = torch._foreach_add(torch._foreach_sqrt(s_ref), eps)
+        torch._foreach_sub_(ref, torch._foreach_div(torch._foreach_mul(m_ref, alpha), den))
+        ops.adam_apply(dev, gs, m_dev, s_dev, alpha, b1, b2, eps)
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(dev + m_dev + s_dev, ref + m_ref + s_ref)):
+        a, b = a.cpu(), b.cpu()
+        bad = (a != b).nonzero()
+        assert bad.numel() == 0, (i // len(shapes), i % len(shapes), bad[:3].tolist(),
+                                  a[tuple(bad[0])].item(), b[tuple(bad[0])].item())

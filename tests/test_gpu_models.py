@@ -166,3 +166,20 @@ def test_actor_grads_from_saves_match_tape():
     g_split = sp.actor_grads_from(sp.actor_forward(data))
     for a, b in zip(g_split, g_tape):
         assert rel_close(a.cpu(), b.cpu(), 1e-12)
+
+
+@pytest.mark.parametrize("name,d", [("LQR", 20), ("VDP", 10), ("EKN", 5)])
+def test_critic_split_grads_match_tape(name, d):
+    """critic_front (V's gradients, dL/dG) + critic_G_back (G's gradients from the saves)
+    equal grad_critic (autograd through the whole critic loss) on the same batch,
+    float64."""
+    cfg = full_config(name, d, N=12, hidden=(40, 40), batch=50, valid=50, td="TD1")
+    bp = getattr(peq, name)(cfg.eqn_config)
+    sp = psol.ActorCriticSolver(cfg, bp, seed=3, sampler="device", graphs=False)
+    data = sp.sample(50, 12)
+    g_tape = sp.grad_critic(data, False, False)
+    front = sp.critic_front(data)
+    g_split = front[0] + sp.critic_G_back(front)
+    assert len(g_split) == len(g_tape)
+    for a, b in zip(g_split, g_tape):
+        assert rel_close(a.cpu(), b.cpu(), 1e-12)
