@@ -14,7 +14,7 @@ HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
              -ffp-contract=off
 EQNS      := lqr lqrvar ekn vdp
 HDRS      := $(wildcard $(CSRC)/*.h) include/dpac.h
-OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_adam.o \
+OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_params.o \
              $(foreach e,$(EQNS),$(OBJDIR)/dpac_eqn_$(e)_f32.o $(OBJDIR)/dpac_eqn_$(e)_f64.o)
 LIB       := $(PKG)/libdpac.so
 
@@ -30,7 +30,7 @@ $(OBJDIR)/dpac_mlp.o: $(CSRC)/dpac_mlp.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/dpac_adam.o: $(CSRC)/dpac_adam.hip $(HDRS)
+$(OBJDIR)/dpac_params.o: $(CSRC)/dpac_params.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

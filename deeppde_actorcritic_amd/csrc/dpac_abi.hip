@@ -28,6 +28,8 @@ int mlp_rows_fwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void
                         void* out, void* save_z, hipStream_t s);
 int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
                         const void* save_z, const void* g_out, void* G, void* g_x, hipStream_t s);
+int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
+                       hipStream_t s);
 int adam_launch(int dtype, int n, const int64_t* numel, void* const* var, const void* const* grad,
                 void* const* m, void* const* v, double alpha, double b1, double b2, double eps,
                 hipStream_t s);
@@ -624,6 +626,19 @@ int dpac_equation_eval(const dpac_eqn_params* eq, int32_t what, int32_t dtype, i
   a.what = what; a.dtype = dtype; a.B = num_sample; a.N = 1; a.T = 1.0; a.x = x; a.u = u;
   a.out = out; a.stream = (hipStream_t)stream;
   return launch(a);
+}
+
+int dpac_mlp_prepare(int32_t dtype, const dpac_mlp* net, double gamma_scale, void* scales,
+                     void* weight_t, void* stream) {
+  if (int e = check_net(net)) return e;
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
+  DPAC_REQUIRE(scales);
+  if (weight_t)
+    for (int i = 0; i <= net->n_hidden; ++i)
+      if (!net->weight[i]) return fail(DPAC_EINVAL, "weight[%d] is NULL", i);
+  const int r = mlp_prepare_launch(dtype, *net, gamma_scale, scales, weight_t, (hipStream_t)stream);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
 }
 
 int dpac_adam_apply(int32_t dtype, int32_t n_tensors, const int64_t* numel, void* const* var,

@@ -1,0 +1,171 @@
+// dpac_params.hip — kernels on the parameters of the MLPs rather than on
+// trajectories: the derived tensors every MLP kernel reads (dpac_mlp_prepare) and
+// the optimizer step (dpac_adam_apply).
+//
+// Adam: one optimizer step of TF-form Adam over a list of parameter tensors in
+// one launch (the reference's tf.keras Adam, solver.py:16-21, whose
+// ResourceApplyAdam update is):
+//   m   += (g - m)(1 - b1)
+//   v   += (g*g - v)(1 - b2)
+//   var -= (m*alpha) / (sqrt(v) + eps),   alpha = lr*sqrt(1 - b2^t)/(1 - b1^t)
+// Every operation rounds on its own (the library builds with -ffp-contract=off),
+// in the order above, so the result is bitwise that of the same update written
+// as separate elementwise tensor ops.  Each workgroup row (blockIdx.y) owns one
+// tensor; blocks stride over its elements.  Elementwise and HBM-bound: 16 bytes
+// read + 12 written per fp32 element.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "dpac.h"
+
+namespace dpac {
+
+namespace {
+
+constexpr int kAdamMax = 32;  // tensors per launch (kernel-argument struct stays < 2 KiB)
+constexpr int kAdamThreads = 256;
+
+template <typename T>
+struct AdamArgs {
+  int64_t numel[kAdamMax];
+  T* var[kAdamMax];
+  const T* grad[kAdamMax];
+  T* m[kAdamMax];
+  T* v[kAdamMax];
+  T alpha, omb1, omb2, eps;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kAdamThreads) void k_adam(const AdamArgs<T> a) {
+  const int i = blockIdx.y;
+  const int64_t n = a.numel[i];
+  T* __restrict__ var = a.var[i];
+  const T* __restrict__ g = a.grad[i];
+  T* __restrict__ m = a.m[i];
+  T* __restrict__ v = a.v[i];
+  for (int64_t e = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kAdamThreads) {
+    const T ge = g[e];
+    T me = m[e];
+    T ve = v[e];
+    me = me + (ge - me) * a.omb1;
+    ve = ve + (ge * ge - ve) * a.omb2;
+    const T den = sqrt(ve) + a.eps;
+    var[e] = var[e] - (me * a.alpha) / den;
+    m[e] = me;
+    v[e] = ve;
+  }
+}
+
+template <typename T>
+int launch(int n, const int64_t* numel, void* const* var, const void* const* grad, void* const* m,
+           void* const* v, double alpha, double b1, double b2, double eps, hipStream_t s) {
+  for (int base = 0; base < n; base += kAdamMax) {
+    const int cnt = std::min(kAdamMax, n - base);
+    AdamArgs<T> a{};
+    int64_t mx = 1;
+    for (int j = 0; j < cnt; ++j) {
+      a.numel[j] = numel[base + j];
+      a.var[j] = (T*)var[base + j];
+      a.grad[j] = (const T*)grad[base + j];
+      a.m[j] = (T*)m[base + j];
+      a.v[j] = (T*)v[base + j];
+      mx = std::max(mx, a.numel[j]);
+    }
+    a.alpha = (T)alpha;
+    a.omb1 = (T)(1.0 - b1);
+    a.omb2 = (T)(1.0 - b2);
+    a.eps = (T)eps;
+    const unsigned gx = (unsigned)std::min<int64_t>((mx + kAdamThreads - 1) / kAdamThreads, 64);
+    hipLaunchKernelGGL(k_adam<T>, dim3(gx, (unsigned)cnt), dim3(kAdamThreads), 0, s, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
+}
+
+// dpac_mlp_prepare: s_i = gamma_scale * gamma_i for every BN layer (concatenated)
+// and, optionally, wt_i = (W_i ⊙ s_{i+1})^T [w_{i+1}][w_i] for every dense layer
+// (concatenated), the operands the MLP kernels read.  Element-parallel over the
+// concatenation; each output is one multiply (the same rounding as forming
+// gamma_scale*gamma and W*s as tensor ops).
+template <typename T>
+struct PrepArgs {
+  int L, nseg_s;
+  int width[DPAC_MLP_MAX_HIDDEN + 2];
+  const T* gamma[DPAC_MLP_MAX_HIDDEN + 2];
+  const T* W[DPAC_MLP_MAX_HIDDEN + 1];
+  int64_t soff[DPAC_MLP_MAX_HIDDEN + 3];  // offsets of s_i in `scales`
+  int64_t woff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets of wt_i in `wt`
+  T gscale;
+  T* scales;
+  T* wt;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> a) {
+  const int64_t ns = a.soff[a.L + 2];
+  const int64_t nw = a.wt ? a.woff[a.L + 1] : 0;
+  for (int64_t e = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; e < ns + nw;
+       e += (int64_t)gridDim.x * kAdamThreads) {
+    if (e < ns) {
+      int i = 0;
+      while (e >= a.soff[i + 1]) ++i;
+      a.scales[e] = a.gscale * a.gamma[i][e - a.soff[i]];
+    } else {
+      const int64_t f = e - ns;
+      int i = 0;
+      while (f >= a.woff[i + 1]) ++i;
+      const int64_t r = f - a.woff[i];
+      const int K = a.width[i];               // wt_i is [w_{i+1}][w_i]
+      const int64_t j = r / K, k = r % K;     // wt_i[j][k] = W_i[k][j] * s_{i+1}[j]
+      const T sj = a.gscale * a.gamma[i + 1][j];
+      a.wt[f] = a.W[i][k * a.width[i + 1] + j] * sj;
+    }
+  }
+}
+
+template <typename T>
+int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, hipStream_t s) {
+  PrepArgs<T> a{};
+  a.L = net.n_hidden;
+  int64_t so = 0, wo = 0;
+  for (int i = 0; i <= a.L + 1; ++i) {
+    a.width[i] = net.width[i];
+    a.gamma[i] = (const T*)net.bn_scale[i];
+    a.soff[i] = so;
+    so += net.width[i];
+  }
+  a.soff[a.L + 2] = so;
+  for (int i = 0; i <= a.L; ++i) {
+    a.W[i] = (const T*)net.weight[i];
+    a.woff[i] = wo;
+    wo += (int64_t)net.width[i] * net.width[i + 1];
+  }
+  a.woff[a.L + 1] = wo;
+  a.gscale = (T)gscale;
+  a.scales = (T*)scales;
+  a.wt = (T*)wt;
+  const int64_t total = so + (wt ? wo : 0);
+  const unsigned g = (unsigned)std::min<int64_t>((total + kAdamThreads - 1) / kAdamThreads, 1024);
+  hipLaunchKernelGGL(k_mlp_prepare<T>, dim3(g), dim3(kAdamThreads), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
+                       hipStream_t s) {
+  return dtype == DPAC_F64 ? prepare<double>(net, gamma_scale, scales, wt, s)
+                           : prepare<float>(net, gamma_scale, scales, wt, s);
+}
+
+int adam_launch(int dtype, int n, const int64_t* numel, void* const* var, const void* const* grad,
+                void* const* m, void* const* v, double alpha, double b1, double b2, double eps,
+                hipStream_t s) {
+  return dtype == DPAC_F64 ? launch<double>(n, numel, var, grad, m, v, alpha, b1, b2, eps, s)
+                           : launch<float>(n, numel, var, grad, m, v, alpha, b1, b2, eps, s);
+}
+
+}  // namespace dpac

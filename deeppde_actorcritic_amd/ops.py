@@ -135,6 +135,33 @@ class MlpView:
     def supported(self) -> bool:
         return max(self.widths) <= _lib.MLP_MAX_WIDTH
 
+    @property
+    def scales(self):
+        return self.tensors[:len(self.widths)]
+
+
+def mlp_prepare(gam, bet, Ws, b, ekn: bool, want_wt: bool):
+    """A DeepNN's kernel operands from its raw variables in one dpac_mlp_prepare launch:
+    (MlpView with BN scales s_i = rs*gamma_i, wt or None) with wt[i] =
+    (W_i * s_{i+1})^T [w_{i+1}, w_i], the weight_t operand of the backward kernels.
+    Bitwise the products `rs * gamma` and `(W * s).t()` as tensor ops."""
+    ref = gam[0]
+    _require_gpu(*gam, *Ws)
+    widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+    raw = MlpView(gam, bet, Ws, b, ekn)  # bn_scale slots point at the raw gammas
+    kw = dict(dtype=ref.dtype, device=ref.device)
+    S = torch.empty(sum(widths), **kw)
+    nw = [widths[i] * widths[i + 1] for i in range(len(Ws))]
+    WT = torch.empty(sum(nw), **kw) if want_wt else None
+    call("dpac_mlp_prepare", _dtype_id(ref), ctypes.byref(raw.struct), bn_rs_host(ref.dtype),
+         _ptr(S), _ptr(WT), _stream(ref))
+    view = MlpView(list(torch.split(S, widths)), bet, Ws, b, ekn)
+    wt = None
+    if want_wt:
+        offs = np.cumsum([0] + nw).tolist()
+        wt = [WT[offs[i]:offs[i + 1]].view(widths[i + 1], widths[i]) for i in range(len(Ws))]
+    return view, wt
+
 
 def rollout_nn(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor, total_time: float,
                num_steps: int, mlp: MlpView, *, want_u: bool = True, cost_order: int | None = None,
@@ -188,8 +215,7 @@ class _ActorRolloutNN(torch.autograd.Function):
     def forward(ctx, x0, dw, rs, eqp, scheme, T, N, ekn, *params):
         L = (len(params) - 1) // 3 - 1
         gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
-        scales = [rs * g for g in gam]
-        view = MlpView(scales, bet, Ws, b, ekn)
+        view, _ = mlp_prepare(gam, bet, Ws, b, ekn, False)
         x, dt, coef, u, y, disc, (z, flag, disc_t) = rollout_nn(
             eqp, scheme, x0, dw, T, N, view, cost_order=_lib.COST_ACTOR, save=True)
         ctx.save_for_backward(x, u, dw, z, flag, disc_t, rs, *params)
@@ -224,20 +250,21 @@ def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_x
     gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
     B, d = x.shape[1], x.shape[2]
     widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
-    s = [rs * g for g in gam]
+    view, wt = mlp_prepare(gam, bet, Ws, b, ekn, BPTT_MODE == "fused")
+    s = view.scales
     zoff = np.cumsum([0] + widths[1:]).tolist()
     zl = [None] + [z[:, :, zoff[i - 1]:zoff[i]] for i in range(1, L + 2)]
     gx_in = None if g_xN is None else g_xN.contiguous()
     gd_in = None if g_disc is None else g_disc.contiguous()
     gy_in = None if g_y is None else g_y.contiguous()
     if BPTT_MODE == "fused":
-        G = _bptt_fused(eqp, scheme, T, N, ekn, L, x, u, dw, z, flag, disc_t, s, bet, Ws, b,
-                        widths, gx_in, gd_in, gy_in)
+        G = _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, widths,
+                        gx_in, gd_in, gy_in)
     else:
         G = _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b,
                        widths, gx_in, gd_in, gy_in)
     if PARAM_GRADS == "kernel":
-        return mlp_param_grads(MlpView(s, bet, Ws, b, ekn), x[:N].reshape(N * B, d),
+        return mlp_param_grads(view, x[:N].reshape(N * B, d),
                                z.reshape(N * B, -1), G_all(G).reshape(N * B, -1), params)
     # parameter gradients over all N*B rows (PyTorch reference path)
     rows = lambda tt: tt.reshape(N * B, -1)
@@ -319,12 +346,11 @@ def mlp_param_grads(view: "MlpView", x, z, G, like, ws_tag: int = 0):
     return out
 
 
-def _bptt_fused(eqp, scheme, T, N, ekn, L, x, u, dw, z, flag, disc_t, s, bet, Ws, b, widths,
+def _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, widths,
                 g_xN, g_disc, g_y):
-    """G[i] = dL/d(output of BN_i) for every step, [N, B, width[i]], from one launch."""
+    """G[i] = dL/d(output of BN_i) for every step, [N, B, width[i]], from one launch
+    (view, wt from mlp_prepare)."""
     B = x.shape[1]
-    view = MlpView(s, bet, Ws, b, ekn)
-    wt = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]
     wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
     goff = np.cumsum([0] + widths).tolist()
     Gall = torch.empty(N, B, goff[-1], dtype=x.dtype, device=x.device)
@@ -424,7 +450,7 @@ class _RowMLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, rs, *params):
         L, gam, bet, Ws, b = _split_params(params)
-        view = MlpView([rs * g for g in gam], bet, Ws, b, False)
+        view, _ = mlp_prepare(gam, bet, Ws, b, False, False)
         need = any(ctx.needs_input_grad)
         out, z = mlp_rows(view, x, save=need)
         if need:
@@ -445,10 +471,8 @@ def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, w
     want_x) then dpac_mlp_param_grads (if want_params).  params =
     DeepNN.trainable_variables(); returns (g_x or None, parameter gradients or None)."""
     L, gam, bet, Ws, b = _split_params(params)
-    s = [rs * g for g in gam]
-    view = MlpView(s, bet, Ws, b, False)
+    view, wt = mlp_prepare(gam, bet, Ws, b, False, True)
     R = x.shape[0]
-    wt = [(Ws[i] * s[i + 1]).t().contiguous() for i in range(L + 1)]
     wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
     g_x = torch.empty(R, view.widths[0], dtype=x.dtype, device=x.device) if want_x else None
@@ -580,6 +604,20 @@ def td_assemble(eqp, td_type: int, x, u, dw, dt, coef, G=None, *,
                              None if dw is None else dw.contiguous(), dt.contiguous(),
                              coef.contiguous(), eqp, td_type, cost_order, seed, traj_offset,
                              sample_type)
+
+
+def td_assemble_bwd(eqp, x, u, dw, dt, coef, g_y, *, seed: int = 0, traj_offset: int = 0,
+                    sample_type: int = _lib.SAMPLE_NORMAL):
+    """dL/dG [N, B, d] of the TD1 target y (solver.py:177-184) given dL/dy [B] (the
+    backward of td_assemble without autograd)."""
+    _require_gpu(x, u, dw, dt, coef, g_y)
+    B, N = dt.shape
+    gG = torch.empty(N, B, eqp.dim, dtype=x.dtype, device=x.device)
+    call("dpac_td_assemble_bwd", ctypes.byref(eqp), _dtype_id(x), B, N, _ptr(x.contiguous()),
+         _ptr(u.contiguous()), _ptr(None if dw is None else dw.contiguous()),
+         seed & 0xFFFFFFFFFFFFFFFF, traj_offset, sample_type, _ptr(dt.contiguous()),
+         _ptr(coef.contiguous()), _ptr(g_y.contiguous()), _ptr(gG), _stream(x))
+    return gG
 
 
 def actor_cost(eqp, x, u, dt, coef):

@@ -118,9 +118,13 @@ class DeepNN(nn.Module):
     def mlp_view(self):
         """This network as dpac_rollout_nn_fwd reads it (BN scale = rs * gamma, the same
         product forward() forms)."""
-        rs = self.bn_rs
-        return ops.MlpView([rs * g for g in self.bn_gamma], [bt.detach() for bt in self.bn_beta],
-                           [w.detach() for w in self.W], self.b.detach(), self.ekn_head)
+        if not self.bn_rs.is_cuda:
+            rs = self.bn_rs
+            return ops.MlpView([rs * g for g in self.bn_gamma], [bt.detach() for bt in self.bn_beta],
+                               [w.detach() for w in self.W], self.b.detach(), self.ekn_head)
+        view, _ = ops.mlp_prepare([g.detach() for g in self.bn_gamma], [bt.detach() for bt in self.bn_beta],
+                                  [w.detach() for w in self.W], self.b.detach(), self.ekn_head, False)
+        return view
 
     def trainable_variables(self):
         return list(self.bn_gamma) + list(self.bn_beta) + list(self.W) + [self.b]
@@ -376,6 +380,11 @@ class _SplitCriticGraphs:
         return list(self.back_out)
 
 
+def _huber_grad(delta):
+    """d/d delta of the per-sample Huber term of solver.py:76-77."""
+    return torch.where(torch.abs(delta) < DELTA_CLIP, 2 * delta, (2 * DELTA_CLIP) * torch.sign(delta))
+
+
 def _huber_mean(delta):
     """solver.py:76-77 (quadratic inside |delta| < 50, linear outside)."""
     a = torch.abs(delta)
@@ -531,6 +540,15 @@ class ActorCriticSolver(object):
         if self.cheat_value_in_actor:
             term = ops.equation_eval(eqp, _lib.EVAL_V_TRUE, xN)
             gV = ops.equation_eval(eqp, _lib.EVAL_V_GRAD, xN)
+        elif ops.ROW_MLP == "kernel" and self.model_critic.NN_value.fused_ok():
+            # V(x_N) and dV/dx_N (V's parameters are constants here): the row kernels
+            Vnet = self.model_critic.NN_value
+            with torch.no_grad():
+                xN = xN.contiguous()
+                v, zV = ops.mlp_rows(Vnet.mlp_view(), xN, save=True)
+                gV, _ = ops.row_mlp_backward(Vnet.bn_rs, [p.detach() for p in Vnet.trainable_variables()],
+                                             xN, zV, torch.ones_like(v), True, False)
+            term = v[:, 0]
         else:
             xl = xN.detach().requires_grad_(True)
             with torch.enable_grad():
@@ -553,28 +571,38 @@ class ActorCriticSolver(object):
                 and mc.NN_value_grad.fused_ok() and not mc.NN_value_grad.ekn_head)
 
     def critic_front(self, data):
-        """grad_critic's loss (solver.py:73-78) with G = NN_value_grad(x_t) (solver.py:179)
-        evaluated once with saves and entering the tape as a leaf: returns (gradients
-        of V's variables, dL/dG [N*B, d], G's input rows, G's saves)."""
-        mc = self.model_critic
-        net = mc.NN_value_grad
-        held = {}
-
-        def G_fn(xs):
-            rows = xs.reshape(-1, xs.shape[-1])
-            with torch.no_grad():
-                out, z = ops.mlp_rows(net.mlp_view(), rows, save=True)
-            leaf = out.view(xs.shape[0], xs.shape[1], -1).requires_grad_(True)
-            held.update(rows=rows, z=z, leaf=leaf)
-            return leaf
-
+        """grad_critic split at the G network, without autograd: the rollout, G =
+        NN_value_grad(x_t) over the N*B rows with saves (solver.py:179), the TD1 target
+        (solver.py:166-187), V at (x_0, x_N, x_bdry) with saves, then the loss
+        100*(mean h(delta) + mean h(delta_bdry)) (solver.py:73-78, 189-190)
+        differentiated by hand: h'(z) = 2z inside |z| < 50, 100 sign(z) outside;
+        dL/dV(x_0) = g, dL/dV(x_N) = -g*disc, dL/dy = -g, dL/dV(x_bdry) = g_bdry.
+        Returns (gradients of V's variables, dL/dG [N*B, d], G's input rows, G's saves)."""
+        mc, ec = self.model_critic, self.eqn_config
         d = Equation.to_native(data, self.dtype)
-        delta, delta_bdry = mc(d, self.model_actor, False, self.cheat_control_in_critic, G_fn=G_fn)
-        loss = (_huber_mean(delta) + _huber_mean(delta_bdry)) * 100
-        vs = mc.NN_value.trainable_variables()
-        g = torch.autograd.grad(loss, vs + [held["leaf"]], allow_unused=True)
-        gG = g[-1].reshape(held["rows"].shape[0], -1)
-        return list(g[:-1]), gG, held["rows"], held["z"]
+        N, T = ec.num_time_interval_critic, ec.total_time_critic
+        B = d.x0.shape[0]
+        eqp = self.bsde.params()
+        Gnet, Vnet = mc.NN_value_grad, mc.NN_value
+        with torch.no_grad():
+            x, dt, coef, u = self.bsde.rollout(mc.scheme, d.x0, d.dw, T, N, self.model_actor.NN_control,
+                                               cheat=self.cheat_control_in_critic)
+            rows = x[:N].reshape(N * B, -1)
+            G, zG = ops.mlp_rows(Gnet.mlp_view(), rows, save=True)
+            y, disc = ops.td_assemble(eqp, mc.td, x, u, d.dw, dt, coef, G.view(N, B, -1),
+                                      cost_order=_lib.COST_CRITIC)
+            xv = torch.cat([x[0], x[N], d.x_bdry])
+            Vout, zV = ops.mlp_rows(Vnet.mlp_view(), xv, save=True)
+            V = Vout[:, 0]
+            delta = V[:B] - y - V[B:2 * B] * disc                      # solver.py:189
+            delta_b = V[2 * B:] - self.bsde.Z_tf(d.x_bdry)[:, 0]       # solver.py:190
+            g = _huber_grad(delta) * (100.0 / B)
+            g_b = _huber_grad(delta_b) * (100.0 / B)
+            g_out = torch.cat([g, -g * disc, g_b]).unsqueeze(1)
+            _, gV = ops.row_mlp_backward(Vnet.bn_rs, Vnet.trainable_variables(), xv, zV, g_out,
+                                         False, True)
+            gG = ops.td_assemble_bwd(eqp, x, u, d.dw, dt, coef, -g)
+        return gV, gG.reshape(N * B, -1), rows, zG
 
     def critic_G_back(self, front):
         """G's parameter gradients from critic_front's outputs (dpac_mlp_rows_bwd +

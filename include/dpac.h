@@ -310,6 +310,18 @@ int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, doubl
                          const void* x, int64_t ldx, const void* save_z, const void* G,
                          void* workspace, int64_t workspace_bytes, void* grads, void* stream);
 
+/* ---- derived MLP operands --------------------------------------------
+ * The tensors the MLP kernels read, formed from a DeepNN's raw variables in one
+ * launch: with net->bn_scale[i] pointing at the raw BN gamma_i (NOT the scale)
+ * and net->weight[i] at W_i, writes scales = [s_0 | s_1 | ... | s_{L+1}],
+ * s_i = gamma_scale * gamma_i (the inference BatchNormalization scale of
+ * solver.py:246-258, gamma_scale = 1/sqrt(1 + 1e-6)), and, if weight_t is not
+ * NULL, weight_t = [wt_0 | ... | wt_L], wt_i = (W_i ⊙ s_{i+1})^T [width[i+1]][width[i]]
+ * row-major (the weight_t operand of dpac_mlp_rows_bwd / dpac_rollout_nn_bwd).
+ * bn_shift and bias are not read. */
+int dpac_mlp_prepare(int32_t dtype, const dpac_mlp* net, double gamma_scale, void* scales,
+                     void* weight_t, void* stream);
+
 /* ---- optimizer step --------------------------------------------------
  * One step of TF-form Adam (the reference's tf.keras Adam, solver.py:16-21;
  * ResourceApplyAdam) over n_tensors parameter tensors of `dtype`, one launch:

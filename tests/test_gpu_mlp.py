@@ -254,3 +254,23 @@ def test_adam_kernel_matches_foreach_update(dtype):
         bad = (a != b).nonzero()
         assert bad.numel() == 0, (i // len(shapes), i % len(shapes), bad[:3].tolist(),
                                   a[tuple(bad[0])].item(), b[tuple(bad[0])].item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_mlp_prepare_matches_tensor_ops(dtype):
+    """dpac_mlp_prepare gives bitwise rs*gamma_i and (W_i * s_{i+1})^T as tensor ops form them."""
+    widths = (20, 200, 130, 7, 21)
+    gen = torch.Generator().manual_seed(11)
+    gam = [torch.rand(w, generator=gen, dtype=dtype).cuda() for w in widths]
+    bet = [torch.randn(w, generator=gen, dtype=dtype).cuda() for w in widths]
+    Ws = [torch.randn(widths[i], widths[i + 1], generator=gen, dtype=dtype).cuda()
+          for i in range(len(widths) - 1)]
+    b = torch.zeros(widths[-1], dtype=dtype, device="cuda")
+    view, wt = ops.mlp_prepare(gam, bet, Ws, b, False, True)
+    rs = torch.rsqrt(torch.tensor(1.0 + 1e-6, dtype=dtype)).cuda()
+    s = [rs * g for g in gam]
+    for a, e in zip(view.scales, s):
+        assert torch.equal(a, e)
+    for i, w in enumerate(wt):
+        assert torch.equal(w, (Ws[i] * s[i + 1]).t().contiguous())
+    assert view.widths == list(widths)
