@@ -128,10 +128,78 @@ __device__ __forceinline__ void mfma_rows16(const T* in, int K, int Nout, const 
   }
 }
 
+#ifndef DPAC_NN_SPLITK
+#define DPAC_NN_SPLITK 1  // narrow layers (Nout <= 32) split K over all wavefronts
+#endif
+
+// A narrow layer (Nout <= 32, i.e. NT <= 2 column tiles) as a split-K product: a
+// column split would leave all but NT wavefronts idle through a K/4-long
+// dependent MFMA chain (50 x 40 cycles at K = 200).  Wavefront w multiplies the
+// K slice [32w, 32w + 32) for every column tile (8 k-steps: K <= 256; rows past
+// K read 0 through the descriptor, A columns past K are the zero padding), its
+// partial [16 x 32] goes to LDS (`part`, which the layer's output image may
+// serve as: nothing reads it during this layer), and each of the 512 threads
+// sums one output element over the wavefronts in wave order and runs the
+// epilogue on it.
+template <typename T, int NT, class EPI>
+__device__ __forceinline__ void mfma_rows16_splitk(const T* in, int K, int Nout, const T* W,
+                                                   int wave, int lane, EPI& epi, T* part) {
+  static_assert(kNnWaves == 8 && NT <= 2, "16 rows x 32 columns = one element per thread");
+  using MF = Mfma<T>;
+  constexpr int KS = 8;
+  const int col_l = lane & 15, kq = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, (uint32_t)(K * Nout * (int)sizeof(T)));
+  // this thread's output element and its epilogue constants (latency hidden below)
+  const int tid = wave * 64 + lane, erow = tid >> 5, ecol = tid & 31;
+  const bool evalid = ecol < Nout;
+  const typename EPI::ColE ce = epi.loadE(erow, ecol, evalid);
+  T b[KS][NT], av[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int k = (wave * KS + ks) * 4 + kq;
+    av[ks] = k < K ? in[col_l * kNnLd + k] : T(0);  // the image past K may hold a wider layer's data
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = j * 16 + col_l;
+      const uint32_t off = col < Nout ? (uint32_t)((k * Nout + col) * (int)sizeof(T)) : kOOB;
+      uint32_t w[sizeof(T) / 4];
+      buf_load_dwords<sizeof(T) / 4>(rW, off, w);
+      __builtin_memcpy(&b[ks][j], &w[0], sizeof(T));
+    }
+  }
+  typename MF::acc_t acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = typename MF::acc_t{0, 0, 0, 0};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = MF::mma(av[ks], b[ks][j], acc[j]);
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[(wave * 16 + MF::row(lane, i)) * 32 + j * 16 + col_l] = acc[j][i];
+  __syncthreads();
+  T v = part[erow * 32 + ecol];
+#pragma unroll
+  for (int w = 1; w < kNnWaves; ++w) v += part[(w * 16 + erow) * 32 + ecol];
+  __syncthreads();  // every partial read before the epilogue overwrites `part`
+  if (ecol < NT * 16) epi.storeE(erow, ecol, evalid, v, ce);
+}
+
 // Run mfma_rows16 with this wave's (wave-uniform) tile count.
 template <typename T, class EPI>
 __device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T* W, int wave,
                                            int lane, EPI& epi) {
+#if DPAC_NN_SPLITK
+  if constexpr (kNnWaves == 8) {
+    static_assert(8 * 16 * 32 <= kNnRows * kNnLd, "partials fit the output image");
+    if (Nout <= 32 && K > 32) {  // block-uniform
+      if (Nout <= 16) mfma_rows16_splitk<T, 1>(in, K, Nout, W, wave, lane, epi, epi.out);
+      else mfma_rows16_splitk<T, 2>(in, K, Nout, W, wave, lane, epi, epi.out);
+      return;
+    }
+  }
+#endif
   const int ntiles = (Nout + 15) / 16;
   const int mine = ntiles > wave ? (ntiles - wave + kNnWaves - 1) / kNnWaves : 0;
   static_assert(kNnMaxTilesPerWave <= 4, "dispatch below covers 1..4 tiles");
@@ -160,6 +228,12 @@ struct FwdEpi {
   __device__ Col load(int col, bool valid) const {
     return Col{valid ? scale[col] : T(0), valid ? shift[col] : T(0),
                (valid && bias) ? bias[col] : T(0)};
+  }
+  // one element (split-K epilogue): the same constants and arithmetic
+  using ColE = Col;
+  __device__ ColE loadE(int, int col, bool valid) const { return load(col, valid); }
+  __device__ void storeE(int row, int col, bool valid, T z, const ColE& k) const {
+    store(0, row, col, valid, z, k);
   }
   __device__ void store(int, int row, int col, bool valid, T z, const Col& k) const {
     if (save && valid && row < rows_live) save[row * save_stride + col] = z;
@@ -199,6 +273,27 @@ struct BwdEpi {
       }
     }
     return k;
+  }
+  struct ColE {
+    T s, sh, z;
+  };
+  __device__ ColE loadE(int row, int col, bool valid) const {
+    ColE k{};
+    if (scale) {
+      k.s = valid ? scale[col] : T(0);
+      k.sh = valid ? shift[col] : T(0);
+      k.z = (valid && row < rows_live) ? z[row * z_stride + col] : T(0);
+    }
+    return k;
+  }
+  __device__ void storeE(int row, int col, bool valid, T acc, const ColE& k) const {
+    T v = acc;
+    if (scale) {
+      const T yv = k.sh + k.z * k.s;
+      v = acc * (yv > T(0) ? T(2) : T(1));
+    }
+    if (valid && row < rows_live) g[row * g_stride + col] = v;
+    out[row * kNnLd + col] = valid ? v : T(0);
   }
   __device__ void store(int i, int row, int col, bool valid, T acc, const Col& k) const {
     T v = acc;
