@@ -92,8 +92,9 @@ def training_iteration(dtype, iters=8, warmup=3):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1e3
     return {"ms_per_iteration": ms, "batch": B, "horizon": N, "mlp": "20-200-200-200-20",
-            "note": "critic + actor step, HIP-graph replay, fused NN rollouts; the actor's "
-                    "forward rollout overlaps the critic step on a side stream"}
+            "note": "critic + actor step, HIP-graph replay, fused NN rollouts; side streams: the "
+                    "actor's forward rollout beside the critic step, the critic's G-network "
+                    "backward beside the actor's BPTT"}
 
 
 def max_over_ranks(v, world):
