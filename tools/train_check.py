@@ -88,12 +88,14 @@ def main():
     ap.add_argument("--seed", type=int, default=11, help="weight-initialisation seed")
     ap.add_argument("--data-seed", type=int, default=123, help="np.random.seed before train()")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "train_check.json"))
+    ap.add_argument("--graphs", type=int, default=1,
+                    help="1: the production path (HIP graphs, split critic/actor steps on side streams)")
     ap.add_argument("--oracle-from", default=None,
                     help="reuse the oracle history of an earlier train_check JSON (same settings)")
     a = ap.parse_args()
     runs = a.runs.split(",")
     res = {"config": f"{a.config} (configs/{a.config}.json values)", "iters": a.iters, "log_freq": a.log_freq,
-           "batch": a.batch, "valid": a.valid, "runs": {}}
+           "batch": a.batch, "valid": a.valid, "graphs": bool(a.graphs), "runs": {}}
     init = None
     for run in runs:
         if run == "oracle":
@@ -101,7 +103,7 @@ def main():
         dtype = "float32" if run == "gpu32" else "float64"
         cfg = lqr_d20(a.iters, a.log_freq, dtype, a.batch, a.valid, a.config)
         bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
-        sp = psol.ActorCriticSolver(cfg, bsde, seed=a.seed, sampler="host")
+        sp = psol.ActorCriticSolver(cfg, bsde, seed=a.seed, sampler="host", graphs=bool(a.graphs))
         if init is None:  # every run starts from the first run's weights, in float64
             init = {"critic": sp.model_critic.NN_value.export_params(),
                     "critic_grad": sp.model_critic.NN_value_grad.export_params(),
