@@ -97,6 +97,42 @@ def training_iteration(dtype, iters=8, warmup=3):
                     "backward beside the actor's BPTT"}
 
 
+def training_dp(dtype, world, iters=5, warmup=3):
+    """lqr_var_d20 (BASELINE configs[3]: global batch 16384, TD1, N=100, 3x200 MLPs,
+    state-dependent diffusion) trained data-parallel over the ranks: each rank samples and
+    rolls out its contiguous shard of every batch, and each optimiser step all-reduces the
+    flattened gradient once over RCCL (parallel.DataParallel, solver.train_iteration).
+    Strong scaling: the global batch is fixed."""
+    from deeppde_actorcritic_amd import equation as peq
+    from deeppde_actorcritic_amd import solver as psol
+    from deeppde_actorcritic_amd.parallel import DataParallel
+    from tools.train_check import lqr_d20
+    Bg, N = 16384, 100
+    cfg = lqr_d20(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", Bg, Bg,
+                  name="lqr_var_d20")
+    par = DataParallel() if world > 1 else None
+    sp = psol.ActorCriticSolver(cfg, peq.LQR_var(cfg.eqn_config), seed=1, sampler="device", parallel=par)
+
+    def iteration():  # solver.train's loop body on this rank's shards
+        dc = sp.sample(Bg, N)
+        sp.train_iteration(dc, sp.sample(Bg, N), Bg)
+    for _ in range(warmup):
+        iteration()
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        iteration()
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    ms = wall / iters * 1e3
+    return {"config": "lqr_var_d20", "global_batch": Bg, "batch_per_gpu": Bg // world, "horizon": N,
+            "ms_per_iteration": ms, "traj_steps_per_s": 2 * Bg * N / (ms * 1e-3), "scaling": "strong",
+            "collective": (f"one all-reduce ({torch.distributed.get_backend()}; nccl = RCCL over xGMI) of "
+                           "the flattened gradients per optimiser step") if world > 1 else None}
+
+
 def max_over_ranks(v, world):
     if world == 1:
         return v
@@ -158,8 +194,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        # one rank per GPU; DPAC_DIST_BACKEND=gloo lets ranks share a GPU (rehearsal only)
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
+        dist.init_process_group(os.environ.get("DPAC_DIST_BACKEND", "nccl"))
     else:
         torch.cuda.set_device(0)
 
@@ -263,6 +300,8 @@ def main():
                          "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "dpac::k_rollout_nn"}}
         if world == 1 and not args.no_train:
             variants["training_lqr_d20"] = training_iteration(dtype)
+        if not args.no_train:
+            variants["training_dp_lqr_var_d20"] = training_dp(dtype, world)
         out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
