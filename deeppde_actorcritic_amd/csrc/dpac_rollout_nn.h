@@ -27,7 +27,10 @@ constexpr int kNnWaves = DPAC_NN_WAVES;
 constexpr int kNnThreads = 64 * kNnWaves;
 constexpr int kNnLd = DPAC_MLP_MAX_WIDTH + 4;  // LDS row stride (elements)
 constexpr int kNnMaxTilesPerWave = (DPAC_MLP_MAX_WIDTH / 16 + kNnWaves - 1) / kNnWaves;
-constexpr int kNnPrefetch = 8;  // k-steps of B in flight per tile
+#ifndef DPAC_NN_PREFETCH
+#define DPAC_NN_PREFETCH 4  // measured 14.9 -> 14.7 us per step (12, 16: slower)
+#endif
+constexpr int kNnPrefetch = DPAC_NN_PREFETCH;  // k-steps of B in flight per tile
 #ifndef DPAC_NN_ABLATE
 #define DPAC_NN_ABLATE 0  // timing-only builds: 1 = constant weights, 2 = skip the MLP
 #endif
