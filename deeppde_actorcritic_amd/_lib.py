@@ -61,6 +61,7 @@ class Mlp(ctypes.Structure):
         ("bn_shift", ctypes.c_void_p * (MLP_MAX_HIDDEN + 2)),
         ("weight", ctypes.c_void_p * (MLP_MAX_HIDDEN + 1)),
         ("bias", ctypes.c_void_p),
+        ("weight_km", ctypes.c_void_p * (MLP_MAX_HIDDEN + 1)),
     ]
 
 
@@ -98,7 +99,7 @@ SIGNATURES = {
     "dpac_mlp_param_grads_workspace": [_I32, _I64, ctypes.POINTER(Mlp)],
     "dpac_mlp_param_grads": [_I32, _I64, ctypes.POINTER(Mlp), _D, _P, _I64, _P, _P, _P, _I64, _P,
                              _P],
-    "dpac_mlp_prepare": [_I32, ctypes.POINTER(Mlp), _D, _P, _P, _P],
+    "dpac_mlp_prepare": [_I32, ctypes.POINTER(Mlp), _D, _P, _P, _P, _P, _P],
     "dpac_adam_apply": [_I32, _I32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_void_p),
                         ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                         ctypes.POINTER(ctypes.c_void_p), _D, _D, _D, _D, _P],

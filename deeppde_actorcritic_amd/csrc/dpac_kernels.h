@@ -769,7 +769,10 @@ NnMlp<T> nn_mlp(const dpac_mlp& h) {
     if (i > 0) z += m.width[i];
   }
   m.ztot = z;
-  for (int i = 0; i <= m.L; ++i) m.weight[i] = (const T*)h.weight[i];
+  for (int i = 0; i <= m.L; ++i) {
+    m.weight[i] = (const T*)h.weight[i];
+    m.wkm[i] = (const T*)h.weight_km[i];
+  }
   m.bias = (const T*)h.bias;
   return m;
 }
@@ -893,7 +896,10 @@ int run_op(const OpArgs& a) {
         go += m.width[i];
       }
       r.gtot = go;
-      for (int i = 0; i <= m.L; ++i) r.wt[i] = (const T*)a.mlp_wt[i];
+      for (int i = 0; i <= m.L; ++i) {
+        r.wt[i] = (const T*)a.mlp_wt[i];
+        r.wtkm[i] = (const T*)a.mlp.weight_km[i];  // k-major images of wt (dpac.h)
+      }
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
       if (adaptive) hipLaunchKernelGGL((k_rollout_nn_bwd<T, E, D, DPAC_SCHEME_ADAPTIVE>), ngrid, nblock, 0, s, eq, c, m, r);
       else hipLaunchKernelGGL((k_rollout_nn_bwd<T, E, D, DPAC_SCHEME_NAIVE>), ngrid, nblock, 0, s, eq, c, m, r);
@@ -912,7 +918,10 @@ int run_op(const OpArgs& a) {
         if (i > 0) z += m.width[i];
       }
       m.ztot = z;
-      for (int i = 0; i <= m.L; ++i) m.weight[i] = (const T*)a.mlp.weight[i];
+      for (int i = 0; i <= m.L; ++i) {
+        m.weight[i] = (const T*)a.mlp.weight[i];
+        m.wkm[i] = (const T*)a.mlp.weight_km[i];
+      }
       m.bias = (const T*)a.mlp.bias;
       NnRolloutArgs<T> r{};
       r.B = a.B; r.N = a.N; r.cost_order = a.cost_order;

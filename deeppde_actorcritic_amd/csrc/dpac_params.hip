@@ -86,34 +86,42 @@ int launch(int n, const int64_t* numel, void* const* var, const void* const* gra
 }
 
 // dpac_mlp_prepare: s_i = gamma_scale * gamma_i for every BN layer (concatenated)
-// and, optionally, wt_i = (W_i ⊙ s_{i+1})^T [w_{i+1}][w_i] for every dense layer
-// (concatenated), the operands the MLP kernels read.  Element-parallel over the
-// concatenation; each output is one multiply (the same rounding as forming
-// gamma_scale*gamma and W*s as tensor ops).
+// and, optionally, for every dense layer (each segment concatenated over i):
+//   wt_i  = (W_i ⊙ s_{i+1})^T         [w_{i+1}][w_i]
+//   km_i  = W_i^T, k-major padded      [w_{i+1}][K16(w_i)]      (forward image)
+//   tkm_i = W_i ⊙ s_{i+1}, padded      [w_i][K16(w_{i+1})]      (backward image)
+// the operands the MLP kernels read.  Element-parallel over the concatenation;
+// each output is one multiply (the same rounding as forming gamma_scale*gamma
+// and W*s as tensor ops) or a copy.
 template <typename T>
 struct PrepArgs {
-  int L, nseg_s;
+  int L;
   int width[DPAC_MLP_MAX_HIDDEN + 2];
   const T* gamma[DPAC_MLP_MAX_HIDDEN + 2];
   const T* W[DPAC_MLP_MAX_HIDDEN + 1];
   int64_t soff[DPAC_MLP_MAX_HIDDEN + 3];  // offsets of s_i in `scales`
   int64_t woff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets of wt_i in `wt`
+  int64_t koff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets of km_i in `km`
+  int64_t toff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets of tkm_i in `tkm`
   T gscale;
-  T* scales;
-  T* wt;
+  T *scales, *wt, *km, *tkm;
 };
+
+__device__ __forceinline__ int k16(int k) { return (k + 15) / 16 * 16; }
 
 template <typename T>
 __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> a) {
   const int64_t ns = a.soff[a.L + 2];
   const int64_t nw = a.wt ? a.woff[a.L + 1] : 0;
-  for (int64_t e = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; e < ns + nw;
+  const int64_t nk = a.km ? a.koff[a.L + 1] : 0;
+  const int64_t nt = a.tkm ? a.toff[a.L + 1] : 0;
+  for (int64_t e = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; e < ns + nw + nk + nt;
        e += (int64_t)gridDim.x * kAdamThreads) {
     if (e < ns) {
       int i = 0;
       while (e >= a.soff[i + 1]) ++i;
       a.scales[e] = a.gscale * a.gamma[i][e - a.soff[i]];
-    } else {
+    } else if (e < ns + nw) {
       const int64_t f = e - ns;
       int i = 0;
       while (f >= a.woff[i + 1]) ++i;
@@ -122,15 +130,32 @@ __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> 
       const int64_t j = r / K, k = r % K;     // wt_i[j][k] = W_i[k][j] * s_{i+1}[j]
       const T sj = a.gscale * a.gamma[i + 1][j];
       a.wt[f] = a.W[i][k * a.width[i + 1] + j] * sj;
+    } else if (e < ns + nw + nk) {
+      const int64_t f = e - ns - nw;
+      int i = 0;
+      while (f >= a.koff[i + 1]) ++i;
+      const int64_t r = f - a.koff[i];
+      const int K = a.width[i], KP = k16(K);  // km_i[n][k] = W_i[k][n]
+      const int64_t n = r / KP, k = r % KP;
+      a.km[f] = k < K ? a.W[i][k * a.width[i + 1] + n] : T(0);
+    } else {
+      const int64_t f = e - ns - nw - nk;
+      int i = 0;
+      while (f >= a.toff[i + 1]) ++i;
+      const int64_t r = f - a.toff[i];
+      const int K = a.width[i + 1], KP = k16(K);  // tkm_i[n][k] = W_i[n][k] * s_{i+1}[k]
+      const int64_t n = r / KP, k = r % KP;
+      a.tkm[f] = k < K ? a.W[i][n * K + k] * (a.gscale * a.gamma[i + 1][k]) : T(0);
     }
   }
 }
 
 template <typename T>
-int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, hipStream_t s) {
+int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, void* km, void* tkm,
+            hipStream_t s) {
   PrepArgs<T> a{};
   a.L = net.n_hidden;
-  int64_t so = 0, wo = 0;
+  int64_t so = 0, wo = 0, ko = 0, to = 0;
   for (int i = 0; i <= a.L + 1; ++i) {
     a.width[i] = net.width[i];
     a.gamma[i] = (const T*)net.bn_scale[i];
@@ -138,16 +163,25 @@ int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, hipStrea
     so += net.width[i];
   }
   a.soff[a.L + 2] = so;
+  auto pad16 = [](int k) { return (int64_t)((k + 15) / 16 * 16); };
   for (int i = 0; i <= a.L; ++i) {
     a.W[i] = (const T*)net.weight[i];
     a.woff[i] = wo;
+    a.koff[i] = ko;
+    a.toff[i] = to;
     wo += (int64_t)net.width[i] * net.width[i + 1];
+    ko += (int64_t)net.width[i + 1] * pad16(net.width[i]);
+    to += (int64_t)net.width[i] * pad16(net.width[i + 1]);
   }
   a.woff[a.L + 1] = wo;
+  a.koff[a.L + 1] = ko;
+  a.toff[a.L + 1] = to;
   a.gscale = (T)gscale;
   a.scales = (T*)scales;
   a.wt = (T*)wt;
-  const int64_t total = so + (wt ? wo : 0);
+  a.km = (T*)km;
+  a.tkm = (T*)tkm;
+  const int64_t total = so + (wt ? wo : 0) + (km ? ko : 0) + (tkm ? to : 0);
   const unsigned g = (unsigned)std::min<int64_t>((total + kAdamThreads - 1) / kAdamThreads, 1024);
   hipLaunchKernelGGL(k_mlp_prepare<T>, dim3(g), dim3(kAdamThreads), 0, s, a);
   return (int)hipGetLastError();
@@ -156,9 +190,9 @@ int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, hipStrea
 }  // namespace
 
 int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
-                       hipStream_t s) {
-  return dtype == DPAC_F64 ? prepare<double>(net, gamma_scale, scales, wt, s)
-                           : prepare<float>(net, gamma_scale, scales, wt, s);
+                       void* km, void* tkm, hipStream_t s) {
+  return dtype == DPAC_F64 ? prepare<double>(net, gamma_scale, scales, wt, km, tkm, s)
+                           : prepare<float>(net, gamma_scale, scales, wt, km, tkm, s);
 }
 
 int adam_launch(int dtype, int n, const int64_t* numel, void* const* var, const void* const* grad,

@@ -47,6 +47,7 @@ struct NnMlp {
   const T* scale[DPAC_MLP_MAX_HIDDEN + 2];
   const T* shift[DPAC_MLP_MAX_HIDDEN + 2];
   const T* weight[DPAC_MLP_MAX_HIDDEN + 1];
+  const T* wkm[DPAC_MLP_MAX_HIDDEN + 1];  // k-major images of weight (optional, float)
   const T* bias;
 };
 
@@ -66,9 +67,84 @@ struct NnRolloutArgs {
 // K loop is straight-line MFMA code with no per-tile predicate.
 //   EPI::Col load(col, valid)                       per-column constants (before the K loop)
 //   void store(i, row, col, valid, acc, const Col&) one output element (i: accumulator slot)
+// The same product from a k-major weight image (float): Wkm[n][k] = W[k][n] for
+// k < K, 0 for K <= k < K16 = roundup(K, 16), row stride K16 (dpac_mlp_prepare
+// writes them).  One dwordx4 per lane and tile brings 4 consecutive k of one
+// column, one ds_read_b128 the matching 4 A values, so a group of 4 MFMAs costs 2
+// memory instructions instead of 8: the k of MFMA e of group s in lane quad kq is
+// 16s + 4kq + e (a permutation of the K sum; every k once).  Columns K..K16-1 of
+// the A image are zero or finite leftovers, times a zero B.  Measured 14.7 ->
+// 13.3 us per step (B = 2048) and 58 -> 52 (B = 16384) at lqr_d20's actor shape.
+template <int NT, class EPI>
+__device__ __forceinline__ void mfma_rows16_km(const float* in, int K, int Nout, const float* Wkm,
+                                               int wave, int lane, EPI& epi) {
+  using MF = Mfma<float>;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int col_l = lane & 15, kq = lane >> 4;
+  const int K16 = (K + 15) / 16 * 16, ng = K16 / 16;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wkm, (uint32_t)(Nout * K16 * 4));
+  uint32_t voff[NT];
+  MF::acc_t acc[NT];
+  typename EPI::Col cc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+    const bool valid = col < Nout;
+    voff[j] = valid ? (uint32_t)((col * K16 + 4 * kq) * 4) : kOOB;
+    acc[j] = MF::acc_t{0, 0, 0, 0};
+    cc[j] = epi.load(col, valid);  // issued before the K loop: its latency hides there
+  }
+  const float* arow = in + col_l * kNnLd + 4 * kq;  // 16-byte aligned: kNnLd % 4 == 0
+  // groups past the last read 0 (kOOB); A reads are clamped to the last group
+  auto loadB = [&](int s, int j) {
+    uint32_t w[4];
+    buf_load_dwords<4>(rW, s < ng ? voff[j] + (uint32_t)(s * 64) : kOOB, w);
+    f4 v;
+    __builtin_memcpy(&v, &w[0], 16);
+    return v;
+  };
+  auto loadA = [&](int s) { return *reinterpret_cast<const f4*>(arow + 16 * (s < ng ? s : ng - 1)); };
+  constexpr int PG = 2;  // groups (8 k-steps) of B in flight per tile
+  f4 bq[PG][NT], av[PG];
+#pragma unroll
+  for (int q = 0; q < PG; ++q) {
+    av[q] = loadA(q);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bq[q][j] = loadB(q, j);
+  }
+  for (int s0 = 0; s0 < ng; s0 += PG) {
+    f4 an[PG];
+#pragma unroll
+    for (int q = 0; q < PG; ++q) an[q] = loadA(s0 + PG + q);
+#pragma unroll
+    for (int q = 0; q < PG; ++q) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[j] = MF::mma(av[q][e], bq[q][j][e], acc[j]);
+        bq[q][j] = loadB(s0 + q + PG, j);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PG; ++q) av[q] = an[q];
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) epi.store(i, MF::row(lane, i), col, col < Nout, acc[j][i], cc[j]);
+  }
+}
+
 template <typename T, int NT, class EPI>
-__device__ __forceinline__ void mfma_rows16(const T* in, int K, int Nout, const T* W, int wave,
-                                            int lane, EPI& epi) {
+__device__ __forceinline__ void mfma_rows16(const T* in, int K, int Nout, const T* W, const T* Wkm,
+                                            int wave, int lane, EPI& epi) {
+  if constexpr (sizeof(T) == 4) {
+    if (Wkm) {  // block-uniform
+      mfma_rows16_km<NT>(in, K, Nout, Wkm, wave, lane, epi);
+      return;
+    }
+  }
   using MF = Mfma<T>;
   const int col_l = lane & 15, kq = lane >> 4;
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, (uint32_t)(K * Nout * (int)sizeof(T)));
@@ -191,8 +267,8 @@ __device__ __forceinline__ void mfma_rows16_splitk(const T* in, int K, int Nout,
 
 // Run mfma_rows16 with this wave's (wave-uniform) tile count.
 template <typename T, class EPI>
-__device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T* W, int wave,
-                                           int lane, EPI& epi) {
+__device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T* W, const T* Wkm,
+                                           int wave, int lane, EPI& epi) {
 #if DPAC_NN_SPLITK
   if constexpr (kNnWaves == 8) {
     static_assert(8 * 16 * 32 <= kNnRows * kNnLd, "partials fit the output image");
@@ -207,10 +283,10 @@ __device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T
   const int mine = ntiles > wave ? (ntiles - wave + kNnWaves - 1) / kNnWaves : 0;
   static_assert(kNnMaxTilesPerWave <= 4, "dispatch below covers 1..4 tiles");
   switch (mine) {
-    case 1: mfma_rows16<T, 1>(in, K, Nout, W, wave, lane, epi); break;
-    case 2: mfma_rows16<T, 2>(in, K, Nout, W, wave, lane, epi); break;
-    case 3: mfma_rows16<T, 3>(in, K, Nout, W, wave, lane, epi); break;
-    case 4: mfma_rows16<T, 4>(in, K, Nout, W, wave, lane, epi); break;
+    case 1: mfma_rows16<T, 1>(in, K, Nout, W, Wkm, wave, lane, epi); break;
+    case 2: mfma_rows16<T, 2>(in, K, Nout, W, Wkm, wave, lane, epi); break;
+    case 3: mfma_rows16<T, 3>(in, K, Nout, W, Wkm, wave, lane, epi); break;
+    case 4: mfma_rows16<T, 4>(in, K, Nout, W, Wkm, wave, lane, epi); break;
     default: break;
   }
 }
@@ -318,6 +394,7 @@ struct NnBackArgs {
   const T *g_xN, *g_disc, *g_y;
   T *G, *g_x0;
   const T* wt[DPAC_MLP_MAX_HIDDEN + 1];  // (W_i diag s_{i+1})^T, [width[i+1]][width[i]]
+  const T* wtkm[DPAC_MLP_MAX_HIDDEN + 1];  // their k-major images (optional, float)
   int goff[DPAC_MLP_MAX_HIDDEN + 2];     // column offset of G_i in a G row
   int gtot;
 };
@@ -414,7 +491,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd(const E eq, const
       BwdEpi<T> epi{l >= 1 ? mlp.scale[l] : nullptr, l >= 1 ? mlp.shift[l] : nullptr,
                     a.z + (rowt + row0) * mlp.ztot + mlp.zoff[l], mlp.ztot, rows_live, lane, out,
                     a.G + (rowt + row0) * a.gtot + a.goff[l], a.gtot};
-      mfma_layer<T>(in, mlp.width[l + 1], mlp.width[l], a.wt[l], wave, lane, epi);
+      mfma_layer<T>(in, mlp.width[l + 1], mlp.width[l], a.wt[l], a.wtkm[l], wave, lane, epi);
       __syncthreads();
       in = out;
       pq ^= 1;
@@ -499,7 +576,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
       FwdEpi<T> epi{mlp.scale[l + 1], mlp.shift[l + 1], l == L ? mlp.bias : nullptr, l < L, out,
                     a.save_z ? a.save_z + ((int64_t)t * a.B + row0) * mlp.ztot + mlp.zoff[l + 1] : nullptr,
                     mlp.ztot, rows_live};
-      mfma_layer<T>(in, mlp.width[l], mlp.width[l + 1], mlp.weight[l], wave, lane, epi);
+      mfma_layer<T>(in, mlp.width[l], mlp.width[l + 1], mlp.weight[l], mlp.wkm[l], wave, lane, epi);
       __syncthreads();
       in = out;
       pq ^= 1;

@@ -10,6 +10,7 @@ missing: there is no CPU path in the product.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -113,7 +114,7 @@ class MlpView:
     `tensors` keeps every device buffer the struct points to alive; all must be
     contiguous, on the GPU, in the rollout's dtype."""
 
-    def __init__(self, scales, shifts, weights, bias, ekn_head: bool):
+    def __init__(self, scales, shifts, weights, bias, ekn_head: bool, weights_km=None):
         L = len(weights) - 1
         if not 1 <= L <= _lib.MLP_MAX_HIDDEN:
             raise ValueError(f"the fused rollout supports 1..{_lib.MLP_MAX_HIDDEN} hidden layers, got {L}")
@@ -129,8 +130,19 @@ class MlpView:
         for i in range(L + 2):
             m.bn_scale[i], m.bn_shift[i] = sc[i].data_ptr(), sh[i].data_ptr()
         m.bias = b.data_ptr()
+        if weights_km is not None:  # k-major images (dpac_mlp.weight_km), kept alive here
+            self.tensors += list(weights_km)
+            for i, w in enumerate(weights_km):
+                m.weight_km[i] = w.data_ptr()
         self.struct = m
         self.widths = [m.width[i] for i in range(L + 2)]
+
+    def with_km(self, weights_km):
+        """The same view with other k-major images (the backward's, dpac_rollout_nn_bwd)."""
+        L = len(self.widths) - 2
+        t = self.tensors
+        return MlpView(t[:L + 2], t[L + 2:2 * L + 4], t[2 * L + 4:3 * L + 5], t[3 * L + 5],
+                       bool(self.struct.ekn_head), weights_km)
 
     def supported(self) -> bool:
         return max(self.widths) <= _lib.MLP_MAX_WIDTH
@@ -140,27 +152,49 @@ class MlpView:
         return self.tensors[:len(self.widths)]
 
 
-def mlp_prepare(gam, bet, Ws, b, ekn: bool, want_wt: bool):
+# "on": float networks also get the k-major weight images (dpac_mlp.weight_km) the fused
+# rollout / BPTT read with 4 k per load; "off": the row-major path (test reference).
+WEIGHT_KM = os.environ.get("DPAC_WEIGHT_KM", "on")
+
+
+def _k16(k):
+    return (k + 15) // 16 * 16
+
+
+def mlp_prepare(gam, bet, Ws, b, ekn: bool, want_wt: bool, want_km: bool = True):
     """A DeepNN's kernel operands from its raw variables in one dpac_mlp_prepare launch:
-    (MlpView with BN scales s_i = rs*gamma_i, wt or None) with wt[i] =
+    (MlpView with BN scales s_i = rs*gamma_i, wt or None, wt_km or None) with wt[i] =
     (W_i * s_{i+1})^T [w_{i+1}, w_i], the weight_t operand of the backward kernels.
-    Bitwise the products `rs * gamma` and `(W * s).t()` as tensor ops."""
+    Float networks also get k-major images (want_km, WEIGHT_KM): the view's forward
+    images W_i^T and, with want_wt, wt_km[i] = (W_i * s_{i+1}) padded, for
+    view.with_km(wt_km) in the backward.  Bitwise the products `rs * gamma` and
+    `(W * s).t()` as tensor ops."""
     ref = gam[0]
     _require_gpu(*gam, *Ws)
     widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+    L1 = len(Ws)
     raw = MlpView(gam, bet, Ws, b, ekn)  # bn_scale slots point at the raw gammas
     kw = dict(dtype=ref.dtype, device=ref.device)
+    km = want_km and WEIGHT_KM == "on" and ref.dtype == torch.float32
     S = torch.empty(sum(widths), **kw)
-    nw = [widths[i] * widths[i + 1] for i in range(len(Ws))]
+    nw = [widths[i] * widths[i + 1] for i in range(L1)]
+    nk = [widths[i + 1] * _k16(widths[i]) for i in range(L1)]
+    nt = [widths[i] * _k16(widths[i + 1]) for i in range(L1)]
     WT = torch.empty(sum(nw), **kw) if want_wt else None
+    KM = torch.empty(sum(nk), **kw) if km else None
+    TKM = torch.empty(sum(nt), **kw) if (km and want_wt) else None
     call("dpac_mlp_prepare", _dtype_id(ref), ctypes.byref(raw.struct), bn_rs_host(ref.dtype),
-         _ptr(S), _ptr(WT), _stream(ref))
-    view = MlpView(list(torch.split(S, widths)), bet, Ws, b, ekn)
-    wt = None
-    if want_wt:
-        offs = np.cumsum([0] + nw).tolist()
-        wt = [WT[offs[i]:offs[i + 1]].view(widths[i + 1], widths[i]) for i in range(len(Ws))]
-    return view, wt
+         _ptr(S), _ptr(WT), _ptr(KM), _ptr(TKM), _stream(ref))
+
+    def split(buf, sizes, shapes):
+        offs = np.cumsum([0] + sizes).tolist()
+        return [buf[offs[i]:offs[i + 1]].view(*shapes[i]) for i in range(L1)]
+    km_f = split(KM, nk, [(widths[i + 1], _k16(widths[i])) for i in range(L1)]) if km else None
+    view = MlpView(list(torch.split(S, widths)), bet, Ws, b, ekn, km_f)
+    wt = split(WT, nw, [(widths[i + 1], widths[i]) for i in range(L1)]) if want_wt else None
+    wt_km = split(TKM, nt, [(widths[i], _k16(widths[i + 1])) for i in range(L1)]) \
+        if TKM is not None else None
+    return view, wt, wt_km
 
 
 def rollout_nn(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor, total_time: float,
@@ -215,7 +249,7 @@ class _ActorRolloutNN(torch.autograd.Function):
     def forward(ctx, x0, dw, rs, eqp, scheme, T, N, ekn, *params):
         L = (len(params) - 1) // 3 - 1
         gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
-        view, _ = mlp_prepare(gam, bet, Ws, b, ekn, False)
+        view, _, _ = mlp_prepare(gam, bet, Ws, b, ekn, False)
         x, dt, coef, u, y, disc, (z, flag, disc_t) = rollout_nn(
             eqp, scheme, x0, dw, T, N, view, cost_order=_lib.COST_ACTOR, save=True)
         ctx.save_for_backward(x, u, dw, z, flag, disc_t, rs, *params)
@@ -250,7 +284,7 @@ def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_x
     gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
     B, d = x.shape[1], x.shape[2]
     widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
-    view, wt = mlp_prepare(gam, bet, Ws, b, ekn, BPTT_MODE == "fused")
+    view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, ekn, BPTT_MODE == "fused")
     s = view.scales
     zoff = np.cumsum([0] + widths[1:]).tolist()
     zl = [None] + [z[:, :, zoff[i - 1]:zoff[i]] for i in range(1, L + 2)]
@@ -258,7 +292,8 @@ def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_x
     gd_in = None if g_disc is None else g_disc.contiguous()
     gy_in = None if g_y is None else g_y.contiguous()
     if BPTT_MODE == "fused":
-        G = _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, widths,
+        G = _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t,
+                        view if wt_km is None else view.with_km(wt_km), wt, widths,
                         gx_in, gd_in, gy_in)
     else:
         G = _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b,
@@ -450,7 +485,7 @@ class _RowMLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, rs, *params):
         L, gam, bet, Ws, b = _split_params(params)
-        view, _ = mlp_prepare(gam, bet, Ws, b, False, False)
+        view, _, _ = mlp_prepare(gam, bet, Ws, b, False, False, want_km=False)
         need = any(ctx.needs_input_grad)
         out, z = mlp_rows(view, x, save=need)
         if need:
@@ -471,7 +506,7 @@ def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, w
     want_x) then dpac_mlp_param_grads (if want_params).  params =
     DeepNN.trainable_variables(); returns (g_x or None, parameter gradients or None)."""
     L, gam, bet, Ws, b = _split_params(params)
-    view, wt = mlp_prepare(gam, bet, Ws, b, False, True)
+    view, wt, _ = mlp_prepare(gam, bet, Ws, b, False, True, want_km=False)
     R = x.shape[0]
     wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)

@@ -227,7 +227,13 @@ int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
  *   bn_scale[i] = gamma_i / sqrt(1 + 1e-6), bn_shift[i] = beta_i, [width[i]],
  *     i = 0..n_hidden+1 (BatchNormalization in inference form, solver.py:239-245);
  *   weight[i] = [width[i]][width[i+1]] row-major (x @ W), i = 0..n_hidden;
- *   bias = [out].
+ *   bias = [out];
+ *   weight_km[i] (optional, float only; NULL = not used): the k-major image of
+ *     the i-th product's right operand, [cols][K16] with K16 = roundup(K, 16) and
+ *     zeros for k >= K.  For dpac_rollout_nn_fwd the operand is weight[i]
+ *     (K = width[i], cols = width[i+1]); for dpac_rollout_nn_bwd it is
+ *     weight_t[i] (K = width[i+1], cols = width[i]).  dpac_mlp_prepare writes both.
+ *     The wide layers then load 4 k per lane and instruction.
  * 1 <= n_hidden <= DPAC_MLP_MAX_HIDDEN, every width <= DPAC_MLP_MAX_WIDTH.
  * Outputs as dpac_rollout_fwd, with u [N][B][c] the control actually applied.
  * y/disc (optional, both or neither): the pathwise cost in `cost_order`.
@@ -245,6 +251,7 @@ typedef struct dpac_mlp {
   const void* bn_shift[DPAC_MLP_MAX_HIDDEN + 2];
   const void* weight[DPAC_MLP_MAX_HIDDEN + 1];
   const void* bias;
+  const void* weight_km[DPAC_MLP_MAX_HIDDEN + 1];
 } dpac_mlp;
 
 int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
@@ -318,9 +325,12 @@ int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, doubl
  * solver.py:246-258, gamma_scale = 1/sqrt(1 + 1e-6)), and, if weight_t is not
  * NULL, weight_t = [wt_0 | ... | wt_L], wt_i = (W_i ⊙ s_{i+1})^T [width[i+1]][width[i]]
  * row-major (the weight_t operand of dpac_mlp_rows_bwd / dpac_rollout_nn_bwd).
- * bn_shift and bias are not read. */
+ * Optional k-major images (see dpac_mlp.weight_km), concatenated over i:
+ * weight_km = [W_i^T padded: [width[i+1]][roundup(width[i], 16)]] (forward) and
+ * weight_t_km = [(W_i ⊙ s_{i+1}) padded: [width[i]][roundup(width[i+1], 16)]]
+ * (backward).  bn_shift, bias and net->weight_km are not read. */
 int dpac_mlp_prepare(int32_t dtype, const dpac_mlp* net, double gamma_scale, void* scales,
-                     void* weight_t, void* stream);
+                     void* weight_t, void* weight_km, void* weight_t_km, void* stream);
 
 /* ---- optimizer step --------------------------------------------------
  * One step of TF-form Adam (the reference's tf.keras Adam, solver.py:16-21;

@@ -266,7 +266,7 @@ def test_mlp_prepare_matches_tensor_ops(dtype):
     Ws = [torch.randn(widths[i], widths[i + 1], generator=gen, dtype=dtype).cuda()
           for i in range(len(widths) - 1)]
     b = torch.zeros(widths[-1], dtype=dtype, device="cuda")
-    view, wt = ops.mlp_prepare(gam, bet, Ws, b, False, True)
+    view, wt, wt_km = ops.mlp_prepare(gam, bet, Ws, b, False, True)
     rs = torch.rsqrt(torch.tensor(1.0 + 1e-6, dtype=dtype)).cuda()
     s = [rs * g for g in gam]
     for a, e in zip(view.scales, s):
@@ -274,3 +274,16 @@ def test_mlp_prepare_matches_tensor_ops(dtype):
     for i, w in enumerate(wt):
         assert torch.equal(w, (Ws[i] * s[i + 1]).t().contiguous())
     assert view.widths == list(widths)
+    k16 = lambda k: (k + 15) // 16 * 16
+    if dtype == torch.float32:  # k-major images: W_i^T and W_i * s_{i+1}, zero-padded K
+        L1 = len(Ws)
+        km = view.tensors[-L1:]
+        for i in range(L1):
+            ref_f = torch.zeros(widths[i + 1], k16(widths[i]), dtype=dtype, device="cuda")
+            ref_f[:, :widths[i]] = Ws[i].t()
+            assert torch.equal(km[i], ref_f)
+            ref_b = torch.zeros(widths[i], k16(widths[i + 1]), dtype=dtype, device="cuda")
+            ref_b[:, :widths[i + 1]] = Ws[i] * s[i + 1]
+            assert torch.equal(wt_km[i], ref_b)
+    else:
+        assert wt_km is None
