@@ -133,7 +133,10 @@ MrArgs<T> mr_args(const dpac_mlp& net, int64_t rows) {
     a.goff[i] = gt;
     gt += net.width[i];
   }
-  for (int i = 0; i <= a.L; ++i) a.weight[i] = (const T*)net.weight[i];
+  for (int i = 0; i <= a.L; ++i) {
+    a.weight[i] = (const T*)net.weight[i];
+    a.wkm[i] = (const T*)net.weight_km[i];
+  }
   a.bias = (const T*)net.bias;
   a.ztot = zt;
   a.gtot = gt;

@@ -45,6 +45,7 @@ struct MrArgs {
   const T* shift[DPAC_MLP_MAX_HIDDEN + 2];
   const T* weight[DPAC_MLP_MAX_HIDDEN + 1];  // forward: W_i [w_i][w_{i+1}]
   const T* wt[DPAC_MLP_MAX_HIDDEN + 1];      // backward: (W_i diag s_{i+1})^T [w_{i+1}][w_i]
+  const T* wkm[DPAC_MLP_MAX_HIDDEN + 1];     // k-major images of weight (fwd) / wt (bwd), optional
   const T* bias;
   int zoff[DPAC_MLP_MAX_HIDDEN + 2], goff[DPAC_MLP_MAX_HIDDEN + 2];
   int ztot, gtot;
@@ -118,12 +119,90 @@ __device__ __forceinline__ void mr_layer_nt(const T* in, int K, int Nout, const 
   epi.template finish<NT>(acc, wave, lane);
 }
 
+// The same product from a k-major weight image (float; dpac_mlp.weight_km): one
+// dwordx4 per lane and tile brings 4 consecutive k of one column and one
+// ds_read_b128 per row tile the matching A values; the k of MFMA e of group s in
+// lane quad kq is 16s + 4kq + e (as mfma_rows16_km in dpac_rollout_nn.h).
+template <int NT, int RT, class EPI>
+__device__ __forceinline__ void mr_layer_nt_km(const float* in, int K, int Nout, const float* Wkm,
+                                               int wave, int lane, EPI& epi) {
+  using MF = Mfma<float>;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int col_l = lane & 15, kq = lane >> 4;
+  const int K16 = (K + 15) / 16 * 16, ng = K16 / 16;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wkm, (uint32_t)(Nout * K16 * 4));
+  uint32_t voff[NT];
+  MF::acc_t acc[RT][NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kMrWaves * j) * 16 + col_l;
+    voff[j] = col < Nout ? (uint32_t)((col * K16 + 4 * kq) * 4) : kOOB;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt][j] = MF::acc_t{0, 0, 0, 0};
+  }
+  const float* arow = in + col_l * kMrLd + 4 * kq;  // 16-byte aligned: kMrLd % 4 == 0
+  auto loadB = [&](int s, int j) {
+    uint32_t w[4];
+    buf_load_dwords<4>(rW, s < ng ? voff[j] + (uint32_t)(s * 64) : kOOB, w);
+    f4 v;
+    __builtin_memcpy(&v, &w[0], 16);
+    return v;
+  };
+  auto loadA = [&](int s, int rt) {
+    return *reinterpret_cast<const f4*>(arow + rt * 16 * kMrLd + 16 * (s < ng ? s : ng - 1));
+  };
+  constexpr int PG = 2;  // groups (8 k-steps) of B in flight per tile
+  f4 bq[PG][NT], av[PG][RT];
+#pragma unroll
+  for (int q = 0; q < PG; ++q) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) av[q][rt] = loadA(q, rt);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bq[q][j] = loadB(q, j);
+  }
+  for (int s0 = 0; s0 < ng; s0 += PG) {
+    f4 an[PG][RT];
+#pragma unroll
+    for (int q = 0; q < PG; ++q)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) an[q][rt] = loadA(s0 + PG + q, rt);
+#pragma unroll
+    for (int q = 0; q < PG; ++q) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) acc[rt][j] = MF::mma(av[q][rt][e], bq[q][j][e], acc[rt][j]);
+        bq[q][j] = loadB(s0 + q + PG, j);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PG; ++q)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) av[q][rt] = an[q][rt];
+  }
+  epi.template finish<NT>(acc, wave, lane);
+}
+
 template <typename T, int RT, class EPI>
-__device__ __forceinline__ void mr_layer(const T* in, int K, int Nout, const T* W, int wave,
-                                         int lane, EPI& epi) {
+__device__ __forceinline__ void mr_layer(const T* in, int K, int Nout, const T* W, const T* Wkm,
+                                         int wave, int lane, EPI& epi) {
   const int ntiles = (Nout + 15) / 16;
   const int mine = ntiles > wave ? (ntiles - wave + kMrWaves - 1) / kMrWaves : 0;
   static_assert(DPAC_MLP_MAX_WIDTH / 16 / kMrWaves == 4, "dispatch below covers 1..4 tiles");
+  if constexpr (sizeof(T) == 4) {
+    if (Wkm) {  // block-uniform
+      switch (mine) {
+        case 1: mr_layer_nt_km<1, RT>(in, K, Nout, Wkm, wave, lane, epi); break;
+        case 2: mr_layer_nt_km<2, RT>(in, K, Nout, Wkm, wave, lane, epi); break;
+        case 3: mr_layer_nt_km<3, RT>(in, K, Nout, Wkm, wave, lane, epi); break;
+        case 4: mr_layer_nt_km<4, RT>(in, K, Nout, Wkm, wave, lane, epi); break;
+        default: break;
+      }
+      return;
+    }
+  }
   switch (mine) {
     case 1: mr_layer_nt<T, 1, RT>(in, K, Nout, W, wave, lane, epi); break;
     case 2: mr_layer_nt<T, 2, RT>(in, K, Nout, W, wave, lane, epi); break;
@@ -251,7 +330,7 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_fwd(const MrArgs<T> a) 
                         Nout, rows_live, s_img[pq ^ 1],
                         a.z ? a.z + row0 * a.ztot + a.zoff[l + 1] : nullptr, a.ztot,
                         a.out + row0 * Nout, Nout};
-    mr_layer<T, RT>(s_img[pq], a.width[l], Nout, a.weight[l], wave, lane, epi);
+    mr_layer<T, RT>(s_img[pq], a.width[l], Nout, a.weight[l], a.wkm[l], wave, lane, epi);
     __syncthreads();
     pq ^= 1;
   }
@@ -283,7 +362,7 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_bwd(const MrArgs<T> a) 
     MrBwdEpi<T, RT> epi{l >= 1 ? a.scale[l] : nullptr, l >= 1 ? a.shift[l] : nullptr,
                         a.z + row0 * a.ztot + a.zoff[l], a.ztot, a.width[l], rows_live,
                         s_img[pq ^ 1], a.G + row0 * a.gtot + a.goff[l], a.gtot};
-    mr_layer<T, RT>(s_img[pq], a.width[l + 1], a.width[l], a.wt[l], wave, lane, epi);
+    mr_layer<T, RT>(s_img[pq], a.width[l + 1], a.width[l], a.wt[l], a.wkm[l], wave, lane, epi);
     __syncthreads();
     pq ^= 1;
   }

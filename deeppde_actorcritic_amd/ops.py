@@ -485,7 +485,7 @@ class _RowMLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, rs, *params):
         L, gam, bet, Ws, b = _split_params(params)
-        view, _, _ = mlp_prepare(gam, bet, Ws, b, False, False, want_km=False)
+        view, _, _ = mlp_prepare(gam, bet, Ws, b, False, False)
         need = any(ctx.needs_input_grad)
         out, z = mlp_rows(view, x, save=need)
         if need:
@@ -506,7 +506,9 @@ def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, w
     want_x) then dpac_mlp_param_grads (if want_params).  params =
     DeepNN.trainable_variables(); returns (g_x or None, parameter gradients or None)."""
     L, gam, bet, Ws, b = _split_params(params)
-    view, wt, _ = mlp_prepare(gam, bet, Ws, b, False, True, want_km=False)
+    view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, False, True)
+    if wt_km is not None:
+        view = view.with_km(wt_km)  # dpac_mlp_rows_bwd reads the images of weight_t
     R = x.shape[0]
     wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)

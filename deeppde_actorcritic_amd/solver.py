@@ -123,8 +123,7 @@ class DeepNN(nn.Module):
             return ops.MlpView([rs * g for g in self.bn_gamma], [bt.detach() for bt in self.bn_beta],
                                [w.detach() for w in self.W], self.b.detach(), self.ekn_head)
         view, _, _ = ops.mlp_prepare([g.detach() for g in self.bn_gamma], [bt.detach() for bt in self.bn_beta],
-                                     [w.detach() for w in self.W], self.b.detach(), self.ekn_head, False,
-                                     want_km=self.AC == "actor")  # only the fused rollout reads them
+                                     [w.detach() for w in self.W], self.b.detach(), self.ekn_head, False)
         return view
 
     def trainable_variables(self):

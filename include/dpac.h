@@ -231,8 +231,9 @@ int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
  *   weight_km[i] (optional, float only; NULL = not used): the k-major image of
  *     the i-th product's right operand, [cols][K16] with K16 = roundup(K, 16) and
  *     zeros for k >= K.  For dpac_rollout_nn_fwd the operand is weight[i]
- *     (K = width[i], cols = width[i+1]); for dpac_rollout_nn_bwd it is
- *     weight_t[i] (K = width[i+1], cols = width[i]).  dpac_mlp_prepare writes both.
+ *     (K = width[i], cols = width[i+1]), as for dpac_mlp_rows_fwd; for
+ *     dpac_rollout_nn_bwd and dpac_mlp_rows_bwd it is weight_t[i] (K = width[i+1],
+ *     cols = width[i]).  dpac_mlp_prepare writes both.
  *     The wide layers then load 4 k per lane and instruction.
  * 1 <= n_hidden <= DPAC_MLP_MAX_HIDDEN, every width <= DPAC_MLP_MAX_WIDTH.
  * Outputs as dpac_rollout_fwd, with u [N][B][c] the control actually applied.
