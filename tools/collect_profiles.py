@@ -15,6 +15,7 @@ import json
 import os
 import shutil
 import statistics
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -33,6 +34,14 @@ def main(tag):
     ks = os.path.join(OUT, "prof_kt", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    ts = os.path.join(OUT, "prof_train", "run_kernel_stats.csv")
+    if os.path.exists(ts):  # lqr_d20 training iteration (tools/train_bench.py)
+        shutil.copy(ts, os.path.join(PROF, f"{tag}_train_kernel_stats.csv"))
+        tl = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "iter_timeline.py"),
+                             os.path.join(OUT, "prof_train", "run_kernel_trace.csv")],
+                            capture_output=True, text=True)
+        if tl.returncode == 0:
+            open(os.path.join(PROF, f"{tag}_train_timeline.txt"), "w").write(tl.stdout)
     bl = os.path.join(OUT, "bench.log")
     if os.path.exists(bl):
         lines = [l for l in open(bl) if l.startswith("{")]
