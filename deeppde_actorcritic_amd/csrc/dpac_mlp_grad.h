@@ -25,13 +25,16 @@
 
 namespace dpac {
 
+#ifndef DPAC_PG_SR
+#define DPAC_PG_SR 16  // rows staged per sub-chunk
+#endif
 constexpr int kPgThreads = 256;
 constexpr int kPgQ = DPAC_MLP_MAX_WIDTH / 64;  // A-stage columns per thread
 
 // Rows staged per sub-chunk (4 row phases of the 4 wavefronts).
 template <typename T>
 struct PgCfg {
-  static constexpr int SR = 16;
+  static constexpr int SR = DPAC_PG_SR;
 };
 
 template <typename T>
