@@ -267,3 +267,39 @@ def test_fp32_four_row_kernel_matches_sixteen_row(name, d, hidden, B, monkeypatc
     assert rel_close(ya[same].cpu(), yb[same].cpu(), 2e-4)
     assert rel_close(sa[0][:, same].cpu(), sb[0][:, same].cpu(), 2e-4)  # saved z
     assert torch.equal(sa[1][:, same], sb[1][:, same])                  # saved flags
+
+
+@pytest.mark.parametrize("name,d,hidden,B", [("LQR", 20, (200, 200, 200), 2048), ("EKN", 10, (48, 130, 33), 300),
+                                             ("VDP", 10, (256, 7), 64)])
+def test_fp32_kmajor_weights_match_row_major(name, d, hidden, B, monkeypatch):
+    """The fused rollout and its BPTT reading the k-major weight images (dpac_mlp.weight_km:
+    dwordx4 B loads, permuted K order) against the row-major path on identical inputs
+    (16-row tiles both): <= 1% of trajectories may flip an exit decision, matched ones
+    agree to 2e-4 (1+|b|); the actor gradients to 2e-3 relative."""
+    N, T = 30, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme="adaptive", dtype="float32")
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, _ = actor_pair(cfg, torch.float32)
+    eqp = ep.params()
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=23, dtype=torch.float32, device=DEV)
+    monkeypatch.setenv("DPAC_NN_TILE", "16")
+    out, grads = {}, {}
+    for km in ("on", "off"):
+        monkeypatch.setattr(ops, "WEIGHT_KM", km)
+        view = net.mlp_view()
+        assert (view.struct.weight_km[0] is not None) == (km == "on")
+        out[km] = ops.rollout_nn(eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, view,
+                                 cost_order=_lib.COST_ACTOR, save=True)
+        y, disc, xN = ops.actor_rollout_nn(eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, net)
+        grads[km] = torch.autograd.grad((y + disc).mean() + xN.sum() * 1e-3, net.trainable_variables())
+    xa, _, ca, ua, ya, _, sa = out["on"]
+    xb, _, cb, ub, yb, _, sb = out["off"]
+    same = torch.all(ca == cb, dim=1).cpu().numpy()
+    assert np.mean(~same) <= 1e-2
+    assert rel_close(xa[:, same].cpu(), xb[:, same].cpu(), 2e-4)
+    assert rel_close(ua[:, same].cpu(), ub[:, same].cpu(), 2e-4)
+    assert rel_close(sa[0][:, same].cpu(), sb[0][:, same].cpu(), 2e-4)
+    if np.all(same):
+        for a, b in zip(grads["on"], grads["off"]):
+            scale = 1 + float(b.abs().max())
+            assert float((a - b).abs().max()) <= 2e-3 * scale
