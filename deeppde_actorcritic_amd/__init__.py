@@ -3,7 +3,9 @@
 Drop-in for MoZhou1995/DeepPDE_ActorCritic's `equation` / `solver` modules:
 the batched boundary-stopped SDE rollout, running-cost accumulation and
 VR-LSTD / LSTD target assembly run as HIP kernels for gfx950 (libdpac.so,
-C ABI in include/dpac.h); the small MLPs and the optimizer run in PyTorch-ROCm.
+C ABI in include/dpac.h), as do the MLPs (MFMA kernels, fused into the actor's
+rollout and BPTT), their parameter gradients and the Adam update; PyTorch-ROCm
+provides device memory, streams, HIP graphs and torch.distributed (RCCL).
 """
 from . import _lib, config, equation, ops, parallel, solver  # noqa: F401
 from .config import load_config, munchify, set_floatx  # noqa: F401

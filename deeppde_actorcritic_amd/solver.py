@@ -2,8 +2,12 @@
 
 `ActorCriticSolver(config, bsde).train()` returns the same 7-tuple as the
 reference (solver.py:71).  The hot path — rollouts, running cost, TD target
-assembly and the per-step backward — runs in libdpac (HIP, gfx950); the small
-MLPs (DeepNN) and the optimizer stay PyTorch-ROCm, as the north star asks.
+assembly and the per-step backward — runs in libdpac (HIP, gfx950), and so do
+the MLPs on the GPU path (fused into the actor's rollout and BPTT, row-parallel
+kernels for the critic's V and G networks, parameter gradients) and the Adam
+update; PyTorch-ROCm holds the parameters, streams, HIP graphs and the
+torch.distributed exchange.  The PyTorch forms of DeepNN stay as test references
+(ops.ROW_MLP / ops.BPTT_MODE / ops.PARAM_GRADS).
 
 Deliberate differences from the reference: the actor MLP is
 evaluated once per step and its output reused for the cost (the reference
