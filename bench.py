@@ -81,8 +81,9 @@ def training_iteration(dtype, iters=8, warmup=3):
     sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=1, sampler="device")
     B, N = 2048, cfg.eqn_config.num_time_interval_critic
     def iteration():  # solver.train's loop body: both samples, critic step, actor step
-        dc = sp.sample(B, N)
-        sp.train_iteration(dc, sp.sample(B, N))
+        dc, da = sp.sample_iteration(B, N, N)
+        sp.train_iteration(dc, da)
+        sp.prefetch_samples(B, N, N)  # the next pair, on a side stream
     for _ in range(warmup):
         iteration()
     torch.cuda.synchronize()
@@ -114,8 +115,9 @@ def training_dp(dtype, world, iters=5, warmup=3):
     sp = psol.ActorCriticSolver(cfg, peq.LQR_var(cfg.eqn_config), seed=1, sampler="device", parallel=par)
 
     def iteration():  # solver.train's loop body on this rank's shards
-        dc = sp.sample(Bg, N)
-        sp.train_iteration(dc, sp.sample(Bg, N), Bg)
+        dc, da = sp.sample_iteration(Bg, N, N)
+        sp.train_iteration(dc, da, Bg)
+        sp.prefetch_samples(Bg, N, N)
     for _ in range(warmup):
         iteration()
     torch.cuda.synchronize()

@@ -455,6 +455,8 @@ class ActorCriticSolver(object):
         else:
             raise ValueError(f"unknown train mode {self.train_config.train!r}")
         self._calls = 0
+        self._next_samples = None  # (spec, critic batch, actor batch, ready event)
+        self._sample_side = None
         self.hip_graphs = (self.sampler == "device") if graphs is None else bool(graphs)
         self._graphs = {}
         self._side = None
@@ -481,6 +483,36 @@ class ActorCriticSolver(object):
         self._calls += 1
         key = (self.seed * 0x9E3779B1 + self._calls) & 0xFFFFFFFFFFFFFFFF
         return self.bsde.sample_device(kind, cnt, N, key, off, self.dtype)
+
+    def sample_iteration(self, num_sample, N_critic, N_actor):
+        """The (critic, actor) samples of one training iteration (solver.py:67-70): the pair
+        prefetch_samples() drew on a side stream if it matches, else drawn now."""
+        spec = (num_sample, N_critic, N_actor)
+        nxt, self._next_samples = self._next_samples, None
+        if nxt is None or nxt[0] != spec:
+            return self.sample(num_sample, N_critic), self.sample(num_sample, N_actor)
+        _, dc, da, ready = nxt
+        cur = torch.cuda.current_stream()
+        cur.wait_event(ready)
+        for t in (*dc, *da):  # made on the side stream, used on this one
+            t.record_stream(cur)
+        return dc, da
+
+    def prefetch_samples(self, num_sample, N_critic, N_actor):
+        """Draw the next iteration's (critic, actor) pair on a side stream (device sampler;
+        the samples do not depend on the parameters), after the current iteration's work is
+        queued, so sampling leaves the critical path.  As long as no other sample() call
+        comes before the next sample_iteration() the Philox keys are those of drawing in
+        place."""
+        if self.sampler != "device":
+            return
+        if self._sample_side is None:
+            self._sample_side = torch.cuda.Stream()
+        with torch.cuda.stream(self._sample_side):  # fresh buffers: nothing to wait for
+            dc, da = self.sample(num_sample, N_critic), self.sample(num_sample, N_actor)
+            ready = torch.cuda.Event()
+            ready.record()
+        self._next_samples = ((num_sample, N_critic, N_actor), dc, da, ready)
 
     # ---- losses ------------------------------------------------------------
     def loss_critic(self, inputs, training, cheat_control):
@@ -775,9 +807,11 @@ class ActorCriticSolver(object):
                 training_history.append([0, 0.0, true_loss_actor, 0.0, 0.0, 0.0, 0.0, 0.0, elapsed_time])
             if self.train_config.train == "actor-critic":
                 # both samples first, in the reference's order (critic, then actor)
-                dc = self.sample(nc.batch_size, ec.num_time_interval_critic)
-                da = self.sample(nc.batch_size, ec.num_time_interval_actor)
+                dc, da = self.sample_iteration(nc.batch_size, ec.num_time_interval_critic,
+                                               ec.num_time_interval_actor)
                 self.train_iteration(dc, da, nc.batch_size)
+                self.prefetch_samples(nc.batch_size, ec.num_time_interval_critic,
+                                      ec.num_time_interval_actor)
             elif self.train_config.train == "critic":
                 self.train_step_critic(self.sample(nc.batch_size, ec.num_time_interval_critic), nc.batch_size)
             else:

@@ -183,3 +183,18 @@ def test_critic_split_grads_match_tape(name, d):
     assert len(g_split) == len(g_tape)
     for a, b in zip(g_split, g_tape):
         assert rel_close(a.cpu(), b.cpu(), 1e-12)
+
+
+def test_sample_iteration_prefetch_keeps_the_sample_stream():
+    """sample_iteration + prefetch_samples (the next iteration's pair drawn on a side stream)
+    return the same batches, bit for bit, as drawing critic then actor samples in place."""
+    cfg = full_config("LQR", 20, N=12, hidden=(16, 16), batch=64, valid=64)
+    a = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=5, sampler="device", graphs=False)
+    b = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=5, sampler="device", graphs=False)
+    for _ in range(3):
+        got = a.sample_iteration(64, 12, 12)
+        a.prefetch_samples(64, 12, 12)
+        ref = (b.sample(64, 12), b.sample(64, 12))
+        for ga, rb in zip(got, ref):
+            for x, y in zip(ga, rb):
+                assert torch.equal(x, y)

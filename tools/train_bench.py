@@ -42,8 +42,9 @@ def main():
         sp.train_step_actor(sp.sample(B, N))
 
     def iteration():  # overlapped: the actor's forward beside the critic step
-        dc = sp.sample(B, N)
-        sp.train_iteration(dc, sp.sample(B, N))
+        dc, da = sp.sample_iteration(B, N, N)
+        sp.train_iteration(dc, da)
+        sp.prefetch_samples(B, N, N)  # the next pair, on a side stream
 
     for _ in range(a.warmup):
         critic()
