@@ -222,37 +222,70 @@ __device__ __forceinline__ void mfma_rows16(const T* in, int K, int Nout, const 
 // epilogue on it.
 template <typename T, int NT, class EPI>
 __device__ __forceinline__ void mfma_rows16_splitk(const T* in, int K, int Nout, const T* W,
-                                                   int wave, int lane, EPI& epi, T* part) {
+                                                   const T* Wkm, int wave, int lane, EPI& epi,
+                                                   T* part) {
   static_assert(kNnWaves == 8 && NT <= 2, "16 rows x 32 columns = one element per thread");
   using MF = Mfma<T>;
   constexpr int KS = 8;
   const int col_l = lane & 15, kq = lane >> 4;
-  const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, (uint32_t)(K * Nout * (int)sizeof(T)));
   // this thread's output element and its epilogue constants (latency hidden below)
   const int tid = wave * 64 + lane, erow = tid >> 5, ecol = tid & 31;
   const bool evalid = ecol < Nout;
   const typename EPI::ColE ce = epi.loadE(erow, ecol, evalid);
-  T b[KS][NT], av[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const int k = (wave * KS + ks) * 4 + kq;
-    av[ks] = k < K ? in[col_l * kNnLd + k] : T(0);  // the image past K may hold a wider layer's data
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int col = j * 16 + col_l;
-      const uint32_t off = col < Nout ? (uint32_t)((k * Nout + col) * (int)sizeof(T)) : kOOB;
-      uint32_t w[sizeof(T) / 4];
-      buf_load_dwords<sizeof(T) / 4>(rW, off, w);
-      __builtin_memcpy(&b[ks][j], &w[0], sizeof(T));
-    }
-  }
   typename MF::acc_t acc[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) acc[j] = typename MF::acc_t{0, 0, 0, 0};
+  bool done = false;
+  if constexpr (sizeof(T) == 4) {
+    if (Wkm) {  // block-uniform: the slice as 2 groups of 16 k from the k-major image
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      const int K16 = (K + 15) / 16 * 16;
+      const __amdgpu_buffer_rsrc_t rK = make_rsrc(Wkm, (uint32_t)(Nout * K16 * 4));
+      f4 bk[2][NT], ak[2];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
+      for (int g = 0; g < 2; ++g) {
+        const int kb = wave * 32 + 16 * g;  // group base; groups at or past K16 read 0
+        ak[g] = kb < K16 ? *reinterpret_cast<const f4*>(in + col_l * kNnLd + kb + 4 * kq)
+                         : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[j] = MF::mma(av[ks], b[ks][j], acc[j]);
+        for (int j = 0; j < NT; ++j) {
+          const int col = j * 16 + col_l;
+          const uint32_t off = (col < Nout && kb < K16) ? (uint32_t)((col * K16 + kb + 4 * kq) * 4) : kOOB;
+          uint32_t w[4];
+          buf_load_dwords<4>(rK, off, w);
+          __builtin_memcpy(&bk[g][j], &w[0], 16);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[j] = MF::mma(ak[g][e], bk[g][j][e], acc[j]);
+      done = true;
+    }
+  }
+  if (!done) {
+    const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, (uint32_t)(K * Nout * (int)sizeof(T)));
+    T b[KS][NT], av[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = (wave * KS + ks) * 4 + kq;
+      av[ks] = k < K ? in[col_l * kNnLd + k] : T(0);  // the image past K may hold a wider layer's data
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int col = j * 16 + col_l;
+        const uint32_t off = col < Nout ? (uint32_t)((k * Nout + col) * (int)sizeof(T)) : kOOB;
+        uint32_t w[sizeof(T) / 4];
+        buf_load_dwords<sizeof(T) / 4>(rW, off, w);
+        __builtin_memcpy(&b[ks][j], &w[0], sizeof(T));
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = MF::mma(av[ks], b[ks][j], acc[j]);
+  }
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -273,8 +306,8 @@ __device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T
   if constexpr (kNnWaves == 8) {
     static_assert(8 * 16 * 32 <= kNnRows * kNnLd, "partials fit the output image");
     if (Nout <= 32 && K > 32) {  // block-uniform
-      if (Nout <= 16) mfma_rows16_splitk<T, 1>(in, K, Nout, W, wave, lane, epi, epi.out);
-      else mfma_rows16_splitk<T, 2>(in, K, Nout, W, wave, lane, epi, epi.out);
+      if (Nout <= 16) mfma_rows16_splitk<T, 1>(in, K, Nout, W, Wkm, wave, lane, epi, epi.out);
+      else mfma_rows16_splitk<T, 2>(in, K, Nout, W, Wkm, wave, lane, epi, epi.out);
       return;
     }
   }
