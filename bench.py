@@ -76,7 +76,7 @@ def training_iteration(dtype, iters=8, warmup=3):
     on on-device samples, the reference's shape: B=2048, N=100, 3x200 MLPs, TD1."""
     from deeppde_actorcritic_amd import equation as peq
     from deeppde_actorcritic_amd import solver as psol
-    from tools.train_check import lqr_d20
+    from deeppde_actorcritic_amd.config import baseline_config as lqr_d20
     cfg = lqr_d20(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", 2048, 2048)
     sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=1, sampler="device")
     B, N = 2048, cfg.eqn_config.num_time_interval_critic
@@ -107,7 +107,7 @@ def training_dp(dtype, world, iters=5, warmup=3):
     from deeppde_actorcritic_amd import equation as peq
     from deeppde_actorcritic_amd import solver as psol
     from deeppde_actorcritic_amd.parallel import DataParallel
-    from tools.train_check import lqr_d20
+    from deeppde_actorcritic_amd.config import baseline_config as lqr_d20
     Bg, N = 16384, 100
     cfg = lqr_d20(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", Bg, Bg,
                   name="lqr_var_d20")
@@ -282,7 +282,7 @@ def main():
             "hbm_GBps_algorithmic": B * N * (3 * d + d + 2) * esize / (pl3 * 1e-3) / 1e9}
         # fused NN-control rollout: actor MLP d-200-200-200-d on MFMA inside the time loop
         from deeppde_actorcritic_amd import solver as psol
-        from tools.train_check import lqr_d20
+        from deeppde_actorcritic_amd.config import baseline_config as lqr_d20
         cfg_nn = lqr_d20(1, 1, "float32" if dtype == torch.float32 else "float64", B, B)
         net = psol.DeepNN(cfg_nn, "actor", torch.Generator().manual_seed(0), dtype, "cuda")
         view = net.mlp_view()

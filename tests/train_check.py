@@ -3,7 +3,7 @@
 (GPU, fp32 and fp64) against the float64 CPU oracle, same initial weights and the
 same host-sampled numpy stream (solver.py:36-71 run verbatim).
 
-    python tools/train_check.py --iters 200 --log-freq 50 --runs gpu32,gpu64,oracle \
+    python tests/train_check.py --iters 200 --log-freq 50 --runs gpu32,gpu64,oracle \
         --out gpurun_out/train_check.json
 
 lqr_d20 is the reference's configs/lqr_d20.json (values restated below): d = c = 20,
@@ -24,35 +24,11 @@ sys.path.insert(0, ROOT)
 
 from deeppde_actorcritic_amd import equation as peq  # noqa: E402
 from deeppde_actorcritic_amd import solver as psol  # noqa: E402
-from deeppde_actorcritic_amd.config import munchify  # noqa: E402
+from deeppde_actorcritic_amd.config import BASELINE_EQN_CONFIGS, baseline_config  # noqa: E402
 
 
-# eqn_config of the reference's BASELINE configs (configs/*.json values restated)
-EQN_CONFIGS = {
-    "lqr_d20": {"_comment": "linear quadratic regulator", "eqn_name": "LQR", "dim": 20, "control_dim": 20,
-                "discount": 1.0, "p": 1.0, "q": 1.0, "beta": 1.0, "R": 1.0},
-    "ekn_d20": {"_comment": "Diffusive Eikonal equation", "eqn_name": "EKN", "dim": 20, "control_dim": 20,
-                "discount": 0, "a2": 1.2, "a3": 0.2, "R": 1.0},
-    "lqr_var_d20": {"_comment": "linear quadratic regulator", "eqn_name": "LQR_var", "dim": 20,
-                    "control_dim": 20, "discount": 1.0, "q": 1.0, "beta": 1.0, "epsilon": 0.01, "R": 1.0},
-    "vdp_d20": {"_comment": "Van Der Pol oscillator", "eqn_name": "VDP", "dim": 20, "control_dim": 10,
-                "discount": 1.0, "a": 1.0, "epsilon": 0.1, "q": 1.0, "R": 1.0},
-}
-
-
-def lqr_d20(iters, log_freq, dtype, batch, valid, name="lqr_d20"):
-    eqn = dict(EQN_CONFIGS[name], total_time_critic=0.2, total_time_actor=0.2,
-               num_time_interval_critic=100, num_time_interval_actor=100)
-    return munchify({
-        "eqn_config": eqn,
-        "net_config": {"num_hiddens_critic": [200, 200, 200], "num_hiddens_actor": [200, 200, 200],
-                       "lr_values_critic": [1e-3, 1e-4, 1e-5], "lr_boundaries_critic": [30000, 40000],
-                       "lr_values_actor": [1e-3, 1e-4, 1e-5], "lr_boundaries_actor": [30000, 40000],
-                       "num_iterations": iters, "batch_size": batch, "valid_size": valid,
-                       "logging_frequency": log_freq, "dtype": dtype, "verbose": False},
-        "train_config": {"sample_type": "normal", "scheme": "adaptive", "TD_type": "TD1",
-                         "train": "actor-critic"},
-    })
+EQN_CONFIGS = BASELINE_EQN_CONFIGS
+lqr_d20 = baseline_config
 
 
 COLS = ["step", "loss_critic", "loss_actor", "err_value", "err_value_infty", "err_control",

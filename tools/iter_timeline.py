@@ -13,8 +13,12 @@ import sys
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_train/run_kernel_trace.csv"
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_sample_dw" in r["Kernel_Name"]]
-a = idx[-2]
+# the last iteration: from the first kernel after the Adam step that precedes its two
+# forward rollouts (its samples were drawn at the end of the previous iteration)
+fwd = [i for i, r in enumerate(rows) if re.search(r"k_rollout_nn4?<", r["Kernel_Name"])]
+t_first = int(rows[fwd[-2]]["Start_Timestamp"])
+adam = [i for i, r in enumerate(rows) if "k_adam" in r["Kernel_Name"] and int(r["End_Timestamp"]) <= t_first]
+a = adam[-1] + 1 if adam else fwd[-2]
 t0 = int(rows[a]["Start_Timestamp"])
 qkey = "Queue_Id" if "Queue_Id" in rows[0] else ("Stream_Id" if "Stream_Id" in rows[0] else None)
 

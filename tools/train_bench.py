@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 
 from deeppde_actorcritic_amd import equation as peq  # noqa: E402
 from deeppde_actorcritic_amd import solver as psol  # noqa: E402
-from tools.train_check import lqr_d20  # noqa: E402
+from deeppde_actorcritic_amd.config import baseline_config as lqr_d20  # noqa: E402
 
 
 def main():
