@@ -34,6 +34,10 @@ constexpr int kNnPrefetch = DPAC_NN_PREFETCH;  // k-steps of B in flight per til
 #ifndef DPAC_NN_ABLATE
 #define DPAC_NN_ABLATE 0  // timing-only builds: 1 = constant weights, 2 = skip the MLP
 #endif
+#ifndef DPAC_BWD_ABLATE
+#define DPAC_BWD_ABLATE 0  // timing-only BPTT builds (bits): 1 = no z loads, 2 = no G stores,
+                           // 4 = no step-lane loads, 8 = skip the MLP chain
+#endif
 // The ring reads A up to k < 4 * roundup(ceil(K/4), kNnPrefetch) <= 256 for K <= 256.
 static_assert(DPAC_MLP_MAX_WIDTH <= 256 && kNnLd >= 256, "A reads stay inside an LDS row");
 
@@ -381,7 +385,11 @@ struct BwdEpi {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = Mfma<T>::row(lane, i);
+#if DPAC_BWD_ABLATE & 1
+        k.z[i] = T(row - col);
+#else
         k.z[i] = (valid && row < rows_live) ? z[row * z_stride + col] : T(0);
+#endif
       }
     }
     return k;
@@ -404,7 +412,9 @@ struct BwdEpi {
       const T yv = k.sh + k.z * k.s;
       v = acc * (yv > T(0) ? T(2) : T(1));
     }
+#if !(DPAC_BWD_ABLATE & 2)
     if (valid && row < rows_live) g[row * g_stride + col] = v;
+#endif
     out[row * kNnLd + col] = valid ? v : T(0);
   }
   __device__ void store(int i, int row, int col, bool valid, T acc, const Col& k) const {
@@ -413,7 +423,9 @@ struct BwdEpi {
       const T yv = k.sh + k.z[i] * k.s;  // the forward's BN_l output, same expression
       v = acc * (yv > T(0) ? T(2) : T(1));  // d(y + relu(y))/dy
     }
+#if !(DPAC_BWD_ABLATE & 2)
     if (valid && row < rows_live) g[row * g_stride + col] = v;
+#endif
     out[row * kNnLd + col] = valid ? v : T(0);
   }
 };
@@ -475,11 +487,21 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd(const E eq, const
     const int64_t rowt = (int64_t)t * a.B;
     if (stepper) {
       T x[M], u[MC], dwv[M], gu[MC], gdn;
+#if DPAC_BWD_ABLATE & 4
+#pragma unroll
+      for (int m = 0; m < M; ++m) x[m] = dwv[m] = T(0.01) * T(m + t);
+#pragma unroll
+      for (int m = 0; m < MC; ++m) u[m] = T(0.02) * T(m - t);
+      const Flags fl = Flags::decode(2 - (t & 1));
+      const T dsc = T(1);
+#else
       own.load_masked(a.x + (rowt + lc.b) * D, x);
       own.load_masked(a.dw + (rowt + lc.b) * D, dwv);
       ownu.load_masked(a.u + (rowt + lc.b) * CD, u);
       const Flags fl = Flags::decode(a.flag[rowt + lc.b]);
-      step_vjp<T, E, SCHEME>(eq, c, x, u, dwv, fl, a.disc_t[rowt + lc.b], lam, gD, gy, gxd, gu, gdn);
+      const T dsc = a.disc_t[rowt + lc.b];
+#endif
+      step_vjp<T, E, SCHEME>(eq, c, x, u, dwv, fl, dsc, lam, gD, gy, gxd, gu, gdn);
       gD = gdn;
       // gradient at the network output, through the Eikonal head (solver.py:272-274)
       T* grow = a.G + (rowt + lc.b) * a.gtot + a.goff[L + 1];
@@ -519,7 +541,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd(const E eq, const
     // ---- input-gradient chain through the MLP (all four wavefronts) ----
     const T* in = s_pq[0];
     int pq = 1;
-    for (int l = L; l >= 0; --l) {
+    for (int l = L; l >= ((DPAC_BWD_ABLATE & 8) ? L + 1 : 0); --l) {
       T* out = s_pq[pq];
       BwdEpi<T> epi{l >= 1 ? mlp.scale[l] : nullptr, l >= 1 ? mlp.shift[l] : nullptr,
                     a.z + (rowt + row0) * mlp.ztot + mlp.zoff[l], mlp.ztot, rows_live, lane, out,
