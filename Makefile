@@ -1,6 +1,6 @@
-# Builds libdpac.so (gfx950) in-tree and the C oracle used as the CPU baseline.
-#   make            -> deeppde_actorcritic_amd/libdpac.so + oracle/_build/liboracle.so
-#   make -j8 lib    -> library only
+# Builds libdpac.so (gfx950) in-tree.  The oracle (oracle/) is Python (torch-CPU float64)
+# and needs no build.
+#   make -j8        -> deeppde_actorcritic_amd/libdpac.so
 HIPCC     ?= /opt/rocm/bin/hipcc
 ARCH      ?= gfx950
 PKG       := deeppde_actorcritic_amd
@@ -18,8 +18,8 @@ OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_params.o \
              $(foreach e,$(EQNS),$(OBJDIR)/dpac_eqn_$(e)_f32.o $(OBJDIR)/dpac_eqn_$(e)_f64.o)
 LIB       := $(PKG)/libdpac.so
 
-.PHONY: all lib oracle clean
-all: lib oracle
+.PHONY: all lib clean
+all: lib
 lib: $(LIB)
 
 $(OBJDIR)/dpac_abi.o: $(CSRC)/dpac_abi.hip $(HDRS)
@@ -45,9 +45,5 @@ $(OBJDIR)/dpac_eqn_%_f64.o: $(CSRC)/dpac_eqn_%.hip $(HDRS)
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
-oracle:
-	$(MAKE) -C oracle
-
 clean:
 	rm -rf build $(LIB)
-	$(MAKE) -C oracle clean

@@ -8,6 +8,10 @@ d = c = 20, B = 4096 trajectories per GPU, N = 200 steps, T = 0.2, adaptive
 scheme, analytic control (the reference's propagate_adaptive with cheat=True,
 equation.py:73-106), increments dw already resident in HBM, writing x [N+1,B,d],
 dt [B,N] and coef [B,N] — the canonical rollout of SURVEY.md §8(d).
+The timed launches rotate over 5 batches (buffer sets of 138 MB each, 690 MB in all), so
+a launch's inputs and outputs are not resident in the 256 MiB Infinity Cache from the
+previous launch: `value` and `roofline` are HBM figures.  The single-set loop (everything
+MALL-resident) is reported as the variant `rollout_mall_resident`.
 Trajectories shard across ranks by global index (weak scaling, no collective on
 the data path).  Rank 0 prints ONE JSON line.
 """
@@ -17,6 +21,7 @@ import argparse
 import ctypes
 import json
 import os
+import platform
 import sys
 import time
 
@@ -28,9 +33,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "SDE trajectory-steps/sec (batch×horizon) at d=20; value-fn rel-L2 vs analytic"
 B_PER_GPU, DIM, HORIZON, T_TOTAL = 4096, 20, 200, 0.2
+N_SETS = 5  # rotating buffer sets: 5 x 138 MB (f32) > the 256 MiB Infinity Cache
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
-BYTES_PER_TRAJ_STEP_F32 = (2 * DIM + 2) * 4  # read dw[d] + write x[d] + dt + coef
+MLP_FLOP_PER_ROW = 2 * (20 * 200 + 200 * 200 * 2 + 200 * 20)  # 176 000
 
 
 def lqr_config():
@@ -53,16 +59,16 @@ def time_launches(launch, steps, warmup, world):
     current stream, which every launch here uses) brackets the same launches:
     per-launch time = event span / steps, i.e. kernel time plus the dispatch gap
     between consecutive launches (rocprofv3's per-kernel average excludes it)."""
-    for _ in range(warmup):
-        launch()
+    for i in range(warmup):
+        launch(i)
     torch.cuda.synchronize()
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     start.record()
-    for _ in range(steps):
-        launch()
+    for i in range(steps):
+        launch(i)
     end.record()
     torch.cuda.synchronize()
     barrier(world)
@@ -71,48 +77,63 @@ def time_launches(launch, steps, warmup, world):
     return wall, per_launch_ms
 
 
-def training_iteration(dtype, iters=8, warmup=3):
-    """End-to-end lqr_d20 training iteration (critic step + actor step, solver.py:67-70)
-    on on-device samples, the reference's shape: B=2048, N=100, 3x200 MLPs, TD1."""
-    from deeppde_actorcritic_amd import equation as peq
-    from deeppde_actorcritic_amd import solver as psol
-    from deeppde_actorcritic_amd.config import baseline_config as lqr_d20
-    cfg = lqr_d20(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", 2048, 2048)
-    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=1, sampler="device")
-    B, N = 2048, cfg.eqn_config.num_time_interval_critic
-    def iteration():  # solver.train's loop body: both samples, critic step, actor step
-        dc, da = sp.sample_iteration(B, N, N)
-        sp.train_iteration(dc, da)
-        sp.prefetch_samples(B, N, N)  # the next pair, on a side stream
-    for _ in range(warmup):
-        iteration()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        iteration()
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / iters * 1e3
-    return {"ms_per_iteration": ms, "batch": B, "horizon": N, "mlp": "20-200-200-200-20",
-            "note": "critic + actor step, HIP-graph replay, fused NN rollouts; side streams: the "
-                    "actor's forward rollout beside the critic step, the critic's G-network "
-                    "backward beside the actor's BPTT"}
+def max_over_ranks(v, world):
+    if world == 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
-def training_dp(dtype, world, iters=5, warmup=3):
-    """lqr_var_d20 (BASELINE configs[3]: global batch 16384, TD1, N=100, 3x200 MLPs,
-    state-dependent diffusion) trained data-parallel over the ranks: each rank samples and
-    rolls out its contiguous shard of every batch, and each optimiser step all-reduces the
-    flattened gradient once over RCCL (parallel.DataParallel, solver.train_iteration).
-    Strong scaling: the global batch is fixed."""
+class RolloutSets:
+    """n buffer sets (x0, dw, x, dt, coef) of this rank's shard and a launcher of
+    dpac_rollout_fwd over set i % n."""
+
+    def __init__(self, lib, eqp, scheme, dtype, B, N, d, off, n):
+        from deeppde_actorcritic_amd import _lib, ops
+        self.lib, self.B, self.N = lib, B, N
+        self.sets = []
+        for i in range(n):
+            x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=1234 + i, traj_offset=off,
+                                   dtype=dtype, device="cuda")
+            x = torch.empty(N + 1, B, d, dtype=dtype, device="cuda")
+            dt = torch.empty(B, N, dtype=dtype, device="cuda")
+            coef = torch.empty(B, N, dtype=dtype, device="cuda")
+            self.sets.append((x0, dw, x, dt, coef))
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        P = ctypes.c_void_p
+        dt_id = _lib.F32 if dtype == torch.float32 else _lib.F64
+        self.args = [(ctypes.byref(eqp), scheme, dt_id, B, N, T_TOTAL, P(x0.data_ptr()), P(dw.data_ptr()),
+                      1234 + i, off, _lib.SAMPLE_NORMAL, P(x.data_ptr()), P(dt.data_ptr()),
+                      P(coef.data_ptr()), None, _lib.COST_CRITIC, None, None, stream)
+                     for i, (x0, dw, x, dt, coef) in enumerate(self.sets)]
+        self.philox_args = [a[:7] + (None,) + a[8:] for a in self.args]
+        self.err = _lib.DpacError
+
+    def launcher(self, nsets, philox=False):
+        fn, args = self.lib.dpac_rollout_fwd, (self.philox_args if philox else self.args)
+
+        def launch(i):
+            rc = fn(*args[i % nsets])
+            if rc:
+                raise self.err("dpac_rollout_fwd", rc, self.lib.dpac_last_error().decode())
+        return launch
+
+
+def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total=None):
+    """One BASELINE config's training iteration (critic step + actor step, solver.py:67-70,
+    one sample pair per iteration; the solver's production path: device sampler, HIP
+    graphs, split critic/actor steps on side streams, MFMA kernels, Adam kernel).
+    B = this rank's batch, total = the global batch (data parallel) or None."""
     from deeppde_actorcritic_amd import equation as peq
     from deeppde_actorcritic_amd import solver as psol
-    from deeppde_actorcritic_amd.parallel import DataParallel
-    from deeppde_actorcritic_amd.config import baseline_config as lqr_d20
-    Bg, N = 16384, 100
-    cfg = lqr_d20(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", Bg, Bg,
-                  name="lqr_var_d20")
-    par = DataParallel() if world > 1 else None
-    sp = psol.ActorCriticSolver(cfg, peq.LQR_var(cfg.eqn_config), seed=1, sampler="device", parallel=par)
+    from deeppde_actorcritic_amd.config import baseline_config
+    Bg = total or B
+    cfg = baseline_config(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", Bg, Bg, name=name)
+    bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
+    sp = psol.ActorCriticSolver(cfg, bsde, seed=1, sampler="device", parallel=par)
+    N = cfg.eqn_config.num_time_interval_critic
 
     def iteration():  # solver.train's loop body on this rank's shards
         dc, da = sp.sample_iteration(Bg, N, N)
@@ -127,56 +148,94 @@ def training_dp(dtype, world, iters=5, warmup=3):
         iteration()
     torch.cuda.synchronize()
     barrier(world)
-    wall = max_over_ranks(time.perf_counter() - t0, world)
-    ms = wall / iters * 1e3
-    return {"config": "lqr_var_d20", "global_batch": Bg, "batch_per_gpu": Bg // world, "horizon": N,
-            "ms_per_iteration": ms, "traj_steps_per_s": 2 * Bg * N / (ms * 1e-3), "scaling": "strong",
-            "collective": (f"one all-reduce ({torch.distributed.get_backend()}; nccl = RCCL over xGMI) of "
-                           "the flattened gradients per optimiser step") if world > 1 else None}
+    ms = max_over_ranks(time.perf_counter() - t0, world) / iters * 1e3
+    # MLP work per iteration: critic ≈ 5, actor ≈ 6 MLP-forward equivalents
+    # per trajectory-step; reported as an achieved rate, not a roofline claim
+    return {"config": name, "global_batch": Bg, "batch_per_gpu": Bg // max(world, 1), "horizon": N,
+            "mlp": "20-200-200-200-%d" % cfg.eqn_config.control_dim, "ms_per_iteration": ms,
+            "traj_steps_per_s": 2 * Bg * N / (ms * 1e-3),
+            "mlp_equiv_TFLOPs": 11 * MLP_FLOP_PER_ROW * Bg * N / (ms * 1e-3) / 1e12}
 
 
-def max_over_ranks(v, world):
-    if world == 1:
-        return v
-    import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+def cpu_info():
+    model = platform.processor() or "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count() or 1
 
 
-def cpu_baseline(seconds=10.0):
-    """Oracle (torch-CPU float64 restatement of equation.py:73-106, cheat=True) on the
-    same workload shape, timed on the host cores (bounded to ~`seconds`)."""
+def cpu_baseline(seconds=8.0):
+    """The oracle (torch-CPU restatement; test infrastructure, timed here only) on the host
+    cores: (i) the canonical rollout (equation.py:73-106, cheat=True) at the bench shape,
+    fp64 and fp32; (ii) one full lqr_d20 training iteration (critic step + actor step,
+    solver.py:67-70) at BASELINE's B = 4096, fp64 and fp32.  Threads = the box's CPU share
+    for one GPU (16; `nproc` counts the whole host).  Bounded samples (about a minute in all)."""
     from oracle import equations as oeq
+    from oracle import precision
+    from oracle import solver as osol
+    from deeppde_actorcritic_amd.config import baseline_config
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    eq = oeq.LQR(lqr_config())
-    np.random.seed(1234)
-    x0, dw, _ = eq.sample_normal(B_PER_GPU, HORIZON)
-    x0t, dwt = torch.as_tensor(x0), torch.as_tensor(dw)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        eq.propagate_adaptive(B_PER_GPU, x0t, dwt, None, False, T_TOTAL, HORIZON, True)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or reps >= 50:
-            break
-    return {"value": reps * B_PER_GPU * HORIZON / el, "unit": "traj-steps/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{reps} x oracle propagate_adaptive(cheat=True), fp64, B={B_PER_GPU}, d={DIM}, "
+    model, nproc = cpu_info()
+    entries = {}
+    for dt in (torch.float64, torch.float32):
+        precision.set_dtype(dt)
+        tag = "f64" if dt == torch.float64 else "f32"
+        eq = oeq.LQR(lqr_config())
+        np.random.seed(1234)
+        x0, dw, _ = eq.sample_normal(B_PER_GPU, HORIZON)
+        x0t, dwt = torch.as_tensor(x0, dtype=dt), torch.as_tensor(dw, dtype=dt)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            eq.propagate_adaptive(B_PER_GPU, x0t, dwt, None, False, T_TOTAL, HORIZON, True)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 50:
+                break
+        entries[f"rollout_{tag}"] = {
+            "value": reps * B_PER_GPU * HORIZON / el, "unit": "traj-steps/s",
+            "sample": f"{reps} x oracle propagate_adaptive(cheat=True), {tag}, B={B_PER_GPU}, d={DIM}, "
                       f"N={HORIZON} ({el:.1f} s)"}
+        Bt = 4096
+        cfg = baseline_config(1, 1, "float64" if dt == torch.float64 else "float32", Bt, Bt, "lqr_d20")
+        eqi = oeq.make(cfg.eqn_config)
+        gen = torch.Generator().manual_seed(1)
+        params = {k: osol.init_params(osol.DeepNN(cfg, ac).sizes, gen)
+                  for k, ac in (("critic", "critic"), ("critic_grad", "critic_grad"), ("actor", "actor"))}
+        so = osol.ActorCriticSolver(cfg, eqi, params=params)
+        np.random.seed(7)
+        dc, da = so.sample(Bt, 100), so.sample(Bt, 100)
+        t0 = time.perf_counter()
+        so.train_step_critic(dc)
+        so.train_step_actor(da)
+        el = time.perf_counter() - t0
+        entries[f"iteration_lqr_d20_{tag}"] = {
+            "value": 2 * Bt * 100 / el, "unit": "traj-steps/s", "ms_per_iteration": el * 1e3,
+            "sample": f"1 oracle training iteration (critic + actor step) on lqr_d20, {tag}, B={Bt}, "
+                      f"N=100, 3x200 MLPs ({el:.1f} s)"}
+    precision.set_dtype(torch.float64)
+    head = entries["rollout_f64"]
+    return {"value": head["value"], "unit": "traj-steps/s", "cores": threads, "kind": "port",
+            "sample": head["sample"] + "; the reference's precision (float64, main.py:35)",
+            "cpu_model": model, "nproc": nproc, "entries": entries}
 
 
 def pmc_traffic(key):
-    """HBM bytes per launch measured by rocprofv3 PMC passes (profiles/pmc_*.json), if present."""
+    """HBM bytes per launch measured by rocprofv3 PMC passes of this bench command
+    (profiles/pmc_traffic.json, written by tools/collect_profiles.py), if present."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     try:
-        d = json.load(open(p))
-        return d.get(key, {}).get("hbm_bytes_per_launch")
+        d = json.load(open(p)).get(key, {})
+        return d.get("hbm_bytes_per_launch"), d.get("source")
     except Exception:
-        return None
+        return None, None
 
 
 def main():
@@ -188,7 +247,7 @@ def main():
     ap.add_argument("--scheme", choices=["adaptive", "naive"], default="adaptive")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
-    ap.add_argument("--no-train", action="store_true", help="skip the training-iteration variant")
+    ap.add_argument("--no-train", action="store_true", help="skip the training-iteration variants")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,99 +270,117 @@ def main():
     scheme = _lib.SCHEME_ADAPTIVE if args.scheme == "adaptive" else _lib.SCHEME_NAIVE
     B, N, d = B_PER_GPU, HORIZON, DIM
     off = rank * B  # this rank's global trajectories [rank*B, rank*B + B)
-    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=1234, traj_offset=off, dtype=dtype,
-                           device="cuda")
-    x = torch.empty(N + 1, B, d, dtype=dtype, device="cuda")
-    dt = torch.empty(B, N, dtype=dtype, device="cuda")
-    coef = torch.empty(B, N, dtype=dtype, device="cuda")
-    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    P = ctypes.c_void_p
-    fn = lib.dpac_rollout_fwd
+    rs = RolloutSets(lib, eqp, scheme, dtype, B, N, d, off, N_SETS)
 
-    def make_launch(dw_ptr):
-        a = (ctypes.byref(eqp), scheme, _lib.F32 if dtype == torch.float32 else _lib.F64, B, N, T_TOTAL,
-             P(x0.data_ptr()), dw_ptr, 1234, off, _lib.SAMPLE_NORMAL, P(x.data_ptr()), P(dt.data_ptr()),
-             P(coef.data_ptr()), None, _lib.COST_CRITIC, None, None, stream)
-
-        def launch():
-            rc = fn(*a)
-            if rc:
-                raise _lib.DpacError("dpac_rollout_fwd", rc, lib.dpac_last_error().decode())
-        return launch
-
-    wall, per_launch_ms = time_launches(make_launch(P(dw.data_ptr())), args.steps, args.warmup, world)
+    wall, per_launch_ms = time_launches(rs.launcher(N_SETS), args.steps, args.warmup, world)
     wall = max_over_ranks(wall, world)
     per_launch_ms = max_over_ranks(per_launch_ms, world)
     ms_per_step = wall / args.steps * 1e3
     value = world * B * N * args.steps / wall
     algo_bytes = B * N * (2 * d + 2) * esize
     achieved = algo_bytes / (per_launch_ms * 1e-3) / 1e9
-    key = f"rollout_{args.scheme}_{args.dtype}_B{B}_N{N}_d{d}"
-    traffic = pmc_traffic(key)
+    traffic, tsrc = pmc_traffic(f"rollout_{args.scheme}_{args.dtype}_B{B}_N{N}_d{d}_cold{N_SETS}")
     out = {
         "metric": METRIC, "value": value, "unit": "traj-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic",
         "config": {"workload": f"canonical rollout, LQR d=20 synthetic: B={B}/GPU, horizon N={N}, "
-                               f"T={T_TOTAL}, {args.scheme} scheme, analytic control, dw resident in HBM",
+                               f"T={T_TOTAL}, {args.scheme} scheme, analytic control, dw resident in HBM; "
+                               f"launches rotate over {N_SETS} batches (not Infinity-Cache resident)",
                    "batch_per_gpu": B, "global_batch": B * world, "dim": d, "horizon": N,
                    "scheme": args.scheme, "parallelism": f"dp{world} (trajectory shards)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "dpac::k_rollout", "algorithmic_bytes_per_launch": algo_bytes,
-                     "avg_launch_ms": per_launch_ms},
+                     "traffic_source": tsrc, "kernel": "dpac::k_rollout",
+                     "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": per_launch_ms},
     }
     if not args.no_variants:
         variants = {}
+        k2 = max(20, args.steps // 4)
+        # the same launch on ONE buffer set: inputs and outputs stay in the Infinity Cache
+        w1, pl1 = time_launches(rs.launcher(1), k2, 5, world)
+        variants["rollout_mall_resident"] = {
+            "traj_steps_per_s": world * B * N * k2 / max_over_ranks(w1, world), "avg_launch_ms": pl1,
+            "GBps_algorithmic": algo_bytes / (pl1 * 1e-3) / 1e9,
+            "frac_of_hbm_peak": algo_bytes / (pl1 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "note": "one 138 MB buffer set re-used every launch (Infinity-Cache resident)"}
         # in-kernel Philox increments (dw not read): 4*(d+2) B per traj-step
-        wall2, pl2 = time_launches(make_launch(None), max(20, args.steps // 4), 5, world)
+        w2, pl2 = time_launches(rs.launcher(N_SETS, philox=True), k2, 5, world)
         variants["rollout_inkernel_philox"] = {
-            "traj_steps_per_s": world * B * N * max(20, args.steps // 4) / max_over_ranks(wall2, world),
+            "traj_steps_per_s": world * B * N * k2 / max_over_ranks(w2, world),
             "avg_launch_ms": pl2, "hbm_GBps_algorithmic": B * N * (d + 2) * esize / (pl2 * 1e-3) / 1e9}
-        # TD1 target assembly over the rolled-out batch: reads x,u,dw,G,dt,coef
+        # the reference's own precision (float64, main.py:35): 336 B per traj-step
+        if dtype == torch.float32:
+            rs64 = RolloutSets(lib, eqp, scheme, torch.float64, B, N, d, off, N_SETS)
+            w5, pl5 = time_launches(rs64.launcher(N_SETS), k2, 5, world)
+            b64 = B * N * (2 * d + 2) * 8
+            variants["rollout_f64"] = {
+                "traj_steps_per_s": world * B * N * k2 / max_over_ranks(w5, world), "avg_launch_ms": pl5,
+                "roofline": {"bound": "hbm", "achieved": b64 / (pl5 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": b64 / (pl5 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "algorithmic_bytes_per_launch": b64},
+                "note": f"float64 (the reference's dtype), {N_SETS} rotating sets of 276 MB"}
+            del rs64
+        # TD1 target assembly over one rolled-out batch: reads x,u,dw,G,dt,coef
+        x0, dw, x, dtb, coef = rs.sets[0]
         u = torch.zeros(N, B, d, dtype=dtype, device="cuda")
         G = torch.randn(N, B, d, dtype=dtype, device="cuda")
         y = torch.empty(B, dtype=dtype, device="cuda")
         disc = torch.empty(B, dtype=dtype, device="cuda")
+        P = ctypes.c_void_p
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         tfn = lib.dpac_td_assemble_fwd
         targs = (ctypes.byref(eqp), _lib.TD1, _lib.COST_CRITIC, _lib.F32 if dtype == torch.float32 else _lib.F64,
-                 B, N, P(x.data_ptr()), P(u.data_ptr()), P(dw.data_ptr()), 0, 0, 0, P(dt.data_ptr()),
+                 B, N, P(x.data_ptr()), P(u.data_ptr()), P(dw.data_ptr()), 0, 0, 0, P(dtb.data_ptr()),
                  P(coef.data_ptr()), P(G.data_ptr()), P(y.data_ptr()), P(disc.data_ptr()), stream)
 
-        def td_launch():
+        def td_launch(i):
             rc = tfn(*targs)
             if rc:
                 raise _lib.DpacError("dpac_td_assemble_fwd", rc, lib.dpac_last_error().decode())
-        k3 = max(20, args.steps // 4)
-        wall3, pl3 = time_launches(td_launch, k3, 5, world)
+        w3, pl3 = time_launches(td_launch, k2, 5, world)
         variants["td1_assembly"] = {
-            "traj_steps_per_s": world * B * N * k3 / max_over_ranks(wall3, world), "avg_launch_ms": pl3,
+            "traj_steps_per_s": world * B * N * k2 / max_over_ranks(w3, world), "avg_launch_ms": pl3,
             "hbm_GBps_algorithmic": B * N * (3 * d + d + 2) * esize / (pl3 * 1e-3) / 1e9}
         # fused NN-control rollout: actor MLP d-200-200-200-d on MFMA inside the time loop
         from deeppde_actorcritic_amd import solver as psol
-        from deeppde_actorcritic_amd.config import baseline_config as lqr_d20
-        cfg_nn = lqr_d20(1, 1, "float32" if dtype == torch.float32 else "float64", B, B)
+        from deeppde_actorcritic_amd.config import baseline_config
+        cfg_nn = baseline_config(1, 1, "float32" if dtype == torch.float32 else "float64", B, B)
         net = psol.DeepNN(cfg_nn, "actor", torch.Generator().manual_seed(0), dtype, "cuda")
         view = net.mlp_view()
         nn_out = {}
 
-        def nn_launch():
+        def nn_launch(i):
             nn_out["r"] = ops.rollout_nn(eqp, scheme, x0, dw, T_TOTAL, N, view, want_u=False)
         k4 = max(5, args.steps // 20)
-        wall4, pl4 = time_launches(nn_launch, k4, 2, world)
-        widths = [d, 200, 200, 200, d]
-        flops = 2 * sum(widths[i] * widths[i + 1] for i in range(4)) * B * N
+        w4, pl4 = time_launches(nn_launch, k4, 2, world)
+        flops = MLP_FLOP_PER_ROW * B * N
         tfs = flops / (pl4 * 1e-3) / 1e12
         variants["rollout_nn_fused"] = {
-            "traj_steps_per_s": world * B * N * k4 / max_over_ranks(wall4, world), "avg_launch_ms": pl4,
-            "mlp": "-".join(map(str, widths)),
+            "traj_steps_per_s": world * B * N * k4 / max_over_ranks(w4, world), "avg_launch_ms": pl4,
+            "mlp": "20-200-200-200-20",
             "roofline": {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "dpac::k_rollout_nn"}}
-        if world == 1 and not args.no_train:
-            variants["training_lqr_d20"] = training_iteration(dtype)
+        del rs, nn_out
+        torch.cuda.empty_cache()
         if not args.no_train:
-            variants["training_dp_lqr_var_d20"] = training_dp(dtype, world)
+            if world == 1:
+                # BASELINE configs[1], [2] (B = 4096 on one GPU), configs[4]'s per-GPU shard of
+                # 65536 over 8 GPUs, and the reference's shipped batch (configs/*.json: 2048)
+                variants["training_lqr_d20"] = training_variant("lqr_d20", dtype, 2048)
+                variants["training_lqr_d20_b4096"] = training_variant("lqr_d20", dtype, 4096)
+                variants["training_ekn_d20_b4096"] = training_variant("ekn_d20", dtype, 4096)
+                variants["training_vdp_d20_b8192"] = training_variant("vdp_d20", dtype, 8192, iters=4)
+            # BASELINE configs[3]: lqr_var_d20, global batch 16384 split over the ranks, one
+            # gradient all-reduce per optimiser step (strong scaling)
+            from deeppde_actorcritic_amd.parallel import DataParallel
+            par = DataParallel() if world > 1 else None
+            v = training_variant("lqr_var_d20", dtype, 16384 // world, world, iters=4, par=par, total=16384)
+            v["scaling"] = "strong"
+            v["collective"] = ((f"one all-reduce ({torch.distributed.get_backend()}; nccl = RCCL over xGMI) "
+                                "of the flattened gradients per optimiser step") if world > 1 else None)
+            variants["training_dp_lqr_var_d20"] = v
         out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()

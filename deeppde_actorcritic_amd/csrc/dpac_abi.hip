@@ -390,7 +390,8 @@ int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
 
 int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
                         int64_t num_sample, int32_t num_steps, double total_time,
-                        const dpac_mlp* actor, const void* const* weight_t, const void* x,
+                        const dpac_mlp* actor, const void* const* weight_t,
+                        const void* const* weight_t_km, const void* x,
                         const void* u, const void* dw, const void* save_z,
                         const int32_t* save_flag, const void* save_disc, const void* g_xN,
                         const void* g_disc, const void* g_y, void* G, void* g_x0,
@@ -411,7 +412,10 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
   OpArgs a = blank(eq, OP_ROLLOUT_NN_BWD);
   a.scheme = scheme; a.dtype = dtype; a.B = num_sample; a.N = num_steps; a.T = total_time;
   a.mlp = *actor;
-  for (int i = 0; i <= actor->n_hidden; ++i) a.mlp_wt[i] = weight_t[i];
+  for (int i = 0; i <= actor->n_hidden; ++i) {
+    a.mlp_wt[i] = weight_t[i];
+    a.mlp.weight_km[i] = weight_t_km ? weight_t_km[i] : nullptr;  // the backward's images
+  }
   a.x = x; a.u = u; a.dw = dw; a.save_z = const_cast<void*>(save_z);
   a.save_flag = const_cast<int32_t*>(save_flag); a.save_disc = const_cast<void*>(save_disc);
   a.g_x_out = g_xN; a.g_disc_out = g_disc; a.g_y_out = g_y; a.g_G = G; a.g_x = g_x0;
@@ -436,7 +440,8 @@ int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
 }
 
 int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* const* weight_t,
-                      const void* save_z, const void* g_out, void* G, void* g_x, void* stream) {
+                      const void* const* weight_t_km, const void* save_z, const void* g_out, void* G,
+                      void* g_x, void* stream) {
   if (int e = check_net(net)) return e;
   if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
   if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1 (got %lld)", (long long)rows);
@@ -446,7 +451,9 @@ int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
   DPAC_REQUIRE(G);
   for (int i = 0; i <= net->n_hidden; ++i)
     if (!weight_t[i]) return fail(DPAC_EINVAL, "weight_t[%d] is NULL", i);
-  const int r = mlp_rows_bwd_launch(dtype, rows, *net, weight_t, save_z, g_out, G, g_x,
+  dpac_mlp bnet = *net;  // the struct's weight_km (forward images) never reach the backward
+  for (int i = 0; i <= net->n_hidden; ++i) bnet.weight_km[i] = weight_t_km ? weight_t_km[i] : nullptr;
+  const int r = mlp_rows_bwd_launch(dtype, rows, bnet, weight_t, save_z, g_out, G, g_x,
                                     (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();

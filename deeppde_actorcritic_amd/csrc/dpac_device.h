@@ -96,43 +96,44 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, kRsrcFlags);
 }
 
-template <int K>
+// AUX: the cache-policy immediate of the buffer instruction (0 = default; 2 = nt).
+template <int K, int AUX = 0>
 __device__ __forceinline__ void buf_load_dwords(__amdgpu_buffer_rsrc_t r, uint32_t voff,
                                                 uint32_t (&w)[K], uint32_t soff = 0) {
   constexpr int k4 = K / 4 * 4;
 #pragma unroll
   for (int k = 0; k < k4; k += 4) {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + 4 * k), (int)soff, 0);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + 4 * k), (int)soff, AUX);
     w[k] = q[0]; w[k + 1] = q[1]; w[k + 2] = q[2]; w[k + 3] = q[3];
   }
   if constexpr (K - k4 == 3) {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(voff + 4 * k4), (int)soff, 0);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b96(r, (int)(voff + 4 * k4), (int)soff, AUX);
     w[k4] = q[0]; w[k4 + 1] = q[1]; w[k4 + 2] = q[2];
   } else if constexpr (K - k4 == 2) {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(voff + 4 * k4), (int)soff, 0);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(voff + 4 * k4), (int)soff, AUX);
     w[k4] = q[0]; w[k4 + 1] = q[1];
   } else if constexpr (K - k4 == 1) {
-    w[k4] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(voff + 4 * k4), (int)soff, 0);
+    w[k4] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(voff + 4 * k4), (int)soff, AUX);
   }
 }
 
-template <int K>
+template <int K, int AUX = 0>
 __device__ __forceinline__ void buf_store_dwords(__amdgpu_buffer_rsrc_t r, uint32_t voff,
                                                  const uint32_t (&w)[K], uint32_t soff = 0) {
   constexpr int k4 = K / 4 * 4;
 #pragma unroll
   for (int k = 0; k < k4; k += 4) {
     __attribute__((ext_vector_type(4))) unsigned int q = {w[k], w[k + 1], w[k + 2], w[k + 3]};
-    __builtin_amdgcn_raw_buffer_store_b128(q, r, (int)(voff + 4 * k), (int)soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(q, r, (int)(voff + 4 * k), (int)soff, AUX);
   }
   if constexpr (K - k4 == 3) {
     __attribute__((ext_vector_type(3))) unsigned int q = {w[k4], w[k4 + 1], w[k4 + 2]};
-    __builtin_amdgcn_raw_buffer_store_b96(q, r, (int)(voff + 4 * k4), (int)soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b96(q, r, (int)(voff + 4 * k4), (int)soff, AUX);
   } else if constexpr (K - k4 == 2) {
     __attribute__((ext_vector_type(2))) unsigned int q = {w[k4], w[k4 + 1]};
-    __builtin_amdgcn_raw_buffer_store_b64(q, r, (int)(voff + 4 * k4), (int)soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(q, r, (int)(voff + 4 * k4), (int)soff, AUX);
   } else if constexpr (K - k4 == 1) {
-    __builtin_amdgcn_raw_buffer_store_b32(w[k4], r, (int)(voff + 4 * k4), (int)soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w[k4], r, (int)(voff + 4 * k4), (int)soff, AUX);
   }
 }
 
@@ -163,31 +164,33 @@ struct BufSlab {
     }
   }
   // soff: wave-uniform byte offset of the row block (the step), in soffset.
+  template <int AUX = 0>
   __device__ void load(__amdgpu_buffer_rsrc_t r, T (&v)[M], uint32_t soff = 0) const {
     if constexpr (kVec) {
       uint32_t w[K];
-      buf_load_dwords<K>(r, off[0], w, soff);
+      buf_load_dwords<K, AUX>(r, off[0], w, soff);
       __builtin_memcpy(&v[0], &w[0], sizeof(w));
     } else {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         uint32_t w[sizeof(T) / 4];
-        buf_load_dwords<sizeof(T) / 4>(r, off[m], w, soff);
+        buf_load_dwords<sizeof(T) / 4, AUX>(r, off[m], w, soff);
         __builtin_memcpy(&v[m], &w[0], sizeof(T));
       }
     }
   }
+  template <int AUX = 0>
   __device__ void store(__amdgpu_buffer_rsrc_t r, const T (&v)[M], uint32_t soff = 0) const {
     if constexpr (kVec) {
       uint32_t w[K];
       __builtin_memcpy(&w[0], &v[0], sizeof(w));
-      buf_store_dwords<K>(r, off[0], w, soff);
+      buf_store_dwords<K, AUX>(r, off[0], w, soff);
     } else {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         uint32_t w[sizeof(T) / 4];
         __builtin_memcpy(&w[0], &v[m], sizeof(T));
-        buf_store_dwords<sizeof(T) / 4>(r, off[m], w, soff);
+        buf_store_dwords<sizeof(T) / 4, AUX>(r, off[m], w, soff);
       }
     }
   }

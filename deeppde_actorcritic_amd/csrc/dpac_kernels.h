@@ -90,11 +90,32 @@ struct DevConsts {
 #ifndef DPAC_RING_VGPRS
 #define DPAC_RING_VGPRS 32
 #endif
+#ifndef DPAC_ROLLOUT_KB_CAP
+#define DPAC_ROLLOUT_KB_CAP 8
+#endif
+// Cache-policy immediates of k_rollout's streamed dw loads and x stores (0 = default).
+#ifndef DPAC_ROLLOUT_DW_AUX
+#define DPAC_ROLLOUT_DW_AUX 0
+#endif
+#ifndef DPAC_ROLLOUT_X_AUX
+#define DPAC_ROLLOUT_X_AUX 0
+#endif
 // KB = 0 (a frame larger than half the budget): no ring, each step loads its
 // own frame right before computing.
 constexpr int ring_kb(int frame_bytes, int budget_vgprs, int cap) {
   const int kb = budget_vgprs * 4 / (2 * frame_bytes);
   return kb > cap ? cap : kb;
+}
+// k_rollout's ring: its dt/coef flush writes F = min(P, 2*KB) steps at compile-time
+// phases of the 2*KB-step period, so F must divide 2*KB and be a power of two (P is).
+// Round KB down to the nearest value that keeps that: a multiple of P/2 when 2*KB >= P
+// (F = P), else a power of two (F = 2*KB).  E.g. P = 8, M = 3: 5 -> 4; P = 4, M = 5: 3 -> 2.
+constexpr int rollout_kb(int kb, int P) {
+  if (kb < 1) kb = 1;
+  if (2 * kb >= P) return kb - kb % (P / 2 > 0 ? P / 2 : 1);
+  int p2 = 1;
+  while (p2 * 2 <= kb) p2 *= 2;
+  return p2;
 }
 // Timing-only ablations (never in a shipped build): 1 = skip the per-step
 // stores of x/dt/coef, 2 = synthesize dw instead of loading it, 3 = skip the
@@ -328,6 +349,8 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
   // F steps (F divides the pipeline period 2*KB, so each unrolled body knows at
   // compile time whether it flushes).
   constexpr int F = P < 2 * KB ? P : 2 * KB;
+  static_assert(KB >= 1 && (2 * KB) % F == 0 && (F & (F - 1)) == 0,
+                "the dt/coef flush needs F | 2*KB and F a power of two (rollout_kb)");
   using TR = Transition<T, E, SCHEME>;
   const LaneCoord<P> lc(a.B, threadIdx.x, xcd_block(blockIdx.x, gridDim.x) * (64 / P));
   const Own<D, P> own(lc.p);
@@ -366,7 +389,7 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
 #pragma unroll
       for (int m = 0; m < M; ++m) fr.dw[m] = T(((t * 7 + m + lc.p) & 3) - 1.5) * T(0.5);
     } else {
-      sx.load(rs_dw, fr.dw, (uint32_t)t * slab);  // zero past d: no mask
+      sx.template load<DPAC_ROLLOUT_DW_AUX>(rs_dw, fr.dw, (uint32_t)t * slab);  // zero past d: no mask
     }
   };
   auto body = [&](int t, DwFrame<T, M>& fr, auto phase) {
@@ -392,7 +415,7 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
       if (t + 1 == a.N) sx.store(rs_x, x, (uint32_t)(t + 1) * slab);
       return;
     }
-    if constexpr (DPAC_ABLATE != 4) sx.store(rs_x, x, (uint32_t)(t + 1) * slab);
+    if constexpr (DPAC_ABLATE != 4) sx.template store<DPAC_ROLLOUT_X_AUX>(rs_x, x, (uint32_t)(t + 1) * slab);
     if constexpr (WANT_U) su.store(rs_u, u, (uint32_t)t * slab_u);
     if constexpr (DPAC_ABLATE != 3) {
       constexpr int PH = decltype(phase)::value;
@@ -808,8 +831,7 @@ int run_op(const OpArgs& a) {
       r.x = (T*)a.x_out; r.dt = (T*)a.dt; r.coef = (T*)a.coef; r.u = (T*)a.u_out;
       r.y = (T*)a.y; r.disc = (T*)a.disc;
       const bool philox = a.dw == nullptr, cost = a.y != nullptr;
-      constexpr int KB_ = ring_kb((int)sizeof(DwFrame<T, E::M>), DPAC_RING_VGPRS, 8);
-      constexpr int KB = KB_ > 0 ? KB_ : 1;
+      constexpr int KB = rollout_kb(ring_kb((int)sizeof(DwFrame<T, E::M>), DPAC_RING_VGPRS, DPAC_ROLLOUT_KB_CAP), E::kP);
       const int out = (cost ? kOutCost : 0) | (a.u_out ? kOutU : 0);
 #define DPAC_ROLL(SCH, PH, OUT) \
   hipLaunchKernelGGL((k_rollout<T, E, D, SCH, PH, OUT, KB>), grid, block, 0, s, eq, c, r)

@@ -74,8 +74,8 @@ int launch(int n, const int64_t* numel, void* const* var, const void* const* gra
       mx = std::max(mx, a.numel[j]);
     }
     a.alpha = (T)alpha;
-    a.omb1 = (T)(1.0 - b1);
-    a.omb2 = (T)(1.0 - b2);
+    a.omb1 = T(1) - (T)b1;  // in T, as ResourceApplyAdam forms (T(1) - beta1())
+    a.omb2 = T(1) - (T)b2;
     a.eps = (T)eps;
     const unsigned gx = (unsigned)std::min<int64_t>((mx + kAdamThreads - 1) / kAdamThreads, 64);
     hipLaunchKernelGGL(k_adam<T>, dim3(gx, (unsigned)cnt), dim3(kAdamThreads), 0, s, a);

@@ -30,7 +30,10 @@ constexpr int kNnMaxTilesPerWave = (DPAC_MLP_MAX_WIDTH / 16 + kNnWaves - 1) / kN
 #ifndef DPAC_NN_PREFETCH
 #define DPAC_NN_PREFETCH 4  // measured 14.9 -> 14.7 us per step (12, 16: slower)
 #endif
-constexpr int kNnPrefetch = DPAC_NN_PREFETCH;  // k-steps of B in flight per tile
+constexpr int kNnPrefetch = DPAC_NN_PREFETCH;
+#ifndef DPAC_NN_KM_PG
+#define DPAC_NN_KM_PG 2  // k-major path: groups of 4 k-steps of B in flight per tile
+#endif  // k-steps of B in flight per tile
 #ifndef DPAC_NN_ABLATE
 #define DPAC_NN_ABLATE 0  // timing-only builds: 1 = constant weights, 2 = skip the MLP
 #endif
@@ -108,7 +111,7 @@ __device__ __forceinline__ void mfma_rows16_km(const float* in, int K, int Nout,
     return v;
   };
   auto loadA = [&](int s) { return *reinterpret_cast<const f4*>(arow + 16 * (s < ng ? s : ng - 1)); };
-  constexpr int PG = 2;  // groups (8 k-steps) of B in flight per tile
+  constexpr int PG = DPAC_NN_KM_PG;  // groups (4 k-steps each) of B in flight per tile
   f4 bq[PG][NT], av[PG];
 #pragma unroll
   for (int q = 0; q < PG; ++q) {

@@ -137,13 +137,6 @@ class MlpView:
         self.struct = m
         self.widths = [m.width[i] for i in range(L + 2)]
 
-    def with_km(self, weights_km):
-        """The same view with other k-major images (the backward's, dpac_rollout_nn_bwd)."""
-        L = len(self.widths) - 2
-        t = self.tensors
-        return MlpView(t[:L + 2], t[L + 2:2 * L + 4], t[2 * L + 4:3 * L + 5], t[3 * L + 5],
-                       bool(self.struct.ekn_head), weights_km)
-
     def supported(self) -> bool:
         return max(self.widths) <= _lib.MLP_MAX_WIDTH
 
@@ -166,8 +159,8 @@ def mlp_prepare(gam, bet, Ws, b, ekn: bool, want_wt: bool, want_km: bool = True)
     (MlpView with BN scales s_i = rs*gamma_i, wt or None, wt_km or None) with wt[i] =
     (W_i * s_{i+1})^T [w_{i+1}, w_i], the weight_t operand of the backward kernels.
     Float networks also get k-major images (want_km, WEIGHT_KM): the view's forward
-    images W_i^T and, with want_wt, wt_km[i] = (W_i * s_{i+1}) padded, for
-    view.with_km(wt_km) in the backward.  Bitwise the products `rs * gamma` and
+    images W_i^T and, with want_wt, wt_km[i] = (W_i * s_{i+1}) padded, the backward entry
+    points' weight_t_km argument.  Bitwise the products `rs * gamma` and
     `(W * s).t()` as tensor ops."""
     ref = gam[0]
     _require_gpu(*gam, *Ws)
@@ -292,8 +285,7 @@ def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_x
     gd_in = None if g_disc is None else g_disc.contiguous()
     gy_in = None if g_y is None else g_y.contiguous()
     if BPTT_MODE == "fused":
-        G = _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t,
-                        view if wt_km is None else view.with_km(wt_km), wt, widths,
+        G = _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km, widths,
                         gx_in, gd_in, gy_in)
     else:
         G = _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b,
@@ -381,17 +373,24 @@ def mlp_param_grads(view: "MlpView", x, z, G, like, ws_tag: int = 0):
     return out
 
 
-def _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, widths,
+def _ptr_array(ts):
+    """A C array of device pointers (NULL for a None list)."""
+    if ts is None:
+        return None
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+def _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km, widths,
                 g_xN, g_disc, g_y):
     """G[i] = dL/d(output of BN_i) for every step, [N, B, width[i]], from one launch
-    (view, wt from mlp_prepare)."""
+    (view, wt, wt_km from mlp_prepare)."""
     B = x.shape[1]
-    wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
     goff = np.cumsum([0] + widths).tolist()
     Gall = torch.empty(N, B, goff[-1], dtype=x.dtype, device=x.device)
     call("dpac_rollout_nn_bwd", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
-         ctypes.byref(view.struct), wt_ptrs, _ptr(x), _ptr(u), _ptr(dw), _ptr(z), _ptr(flag),
-         _ptr(disc_t), _ptr(g_xN), _ptr(g_disc), _ptr(g_y), _ptr(Gall), None, _stream(x))
+         ctypes.byref(view.struct), _ptr_array(wt), _ptr_array(wt_km), _ptr(x), _ptr(u), _ptr(dw),
+         _ptr(z), _ptr(flag), _ptr(disc_t), _ptr(g_xN), _ptr(g_disc), _ptr(g_y), _ptr(Gall), None,
+         _stream(x))
     return [Gall[:, :, goff[i]:goff[i + 1]] for i in range(L + 2)]
 
 
@@ -507,14 +506,11 @@ def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, w
     DeepNN.trainable_variables(); returns (g_x or None, parameter gradients or None)."""
     L, gam, bet, Ws, b = _split_params(params)
     view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, False, True)
-    if wt_km is not None:
-        view = view.with_km(wt_km)  # dpac_mlp_rows_bwd reads the images of weight_t
     R = x.shape[0]
-    wt_ptrs = (ctypes.c_void_p * len(wt))(*[w.data_ptr() for w in wt])
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
     g_x = torch.empty(R, view.widths[0], dtype=x.dtype, device=x.device) if want_x else None
-    call("dpac_mlp_rows_bwd", _dtype_id(x), R, ctypes.byref(view.struct), wt_ptrs, _ptr(z),
-         _ptr(g_out.contiguous()), _ptr(G), _ptr(g_x), _stream(x))
+    call("dpac_mlp_rows_bwd", _dtype_id(x), R, ctypes.byref(view.struct), _ptr_array(wt),
+         _ptr_array(wt_km), _ptr(z), _ptr(g_out.contiguous()), _ptr(G), _ptr(g_x), _stream(x))
     grads = mlp_param_grads(view, x, z, G, params, ws_tag) if want_params else None
     return g_x, grads
 

@@ -70,6 +70,28 @@ class DataParallel:
         for t in tensors:
             dist.broadcast(t.data, src=src, group=self.group)
 
+    def broadcast_int(self, value: int, src: int = 0) -> int:
+        """Rank src's integer on every rank (e.g. a seed drawn on rank 0)."""
+        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+        dist.broadcast(t, src=src, group=self.group)
+        return int(t.item())
+
+    def gather_rows(self, t: torch.Tensor, total: int) -> torch.Tensor:
+        """The ranks' row shards (rank r holds rows shard(total)[r] of a [total, ...] array)
+        concatenated in global row order, on every rank."""
+        counts = [shard_range(total, r, self.world)[1] for r in range(self.world)]
+        if t.shape[0] != counts[self.rank]:
+            raise ValueError(f"gather_rows: rank {self.rank} holds {t.shape[0]} rows, expected "
+                             f"{counts[self.rank]}")
+        dev = t.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        mx = max(counts)
+        buf = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        buf[:t.shape[0]] = t.to(dev)
+        parts = [torch.empty_like(buf) for _ in range(self.world)]
+        dist.all_gather(parts, buf, group=self.group)
+        return torch.cat([p[:c] for p, c in zip(parts, counts)]).to(t.device)
+
 
 class SingleProcess:
     """The same interface for one process (no communication)."""
@@ -90,3 +112,9 @@ class SingleProcess:
 
     def broadcast_(self, tensors, src=0):
         pass
+
+    def broadcast_int(self, value, src=0):
+        return int(value)
+
+    def gather_rows(self, t, total):
+        return t

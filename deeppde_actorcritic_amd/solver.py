@@ -240,10 +240,23 @@ class PiecewiseConstantDecay:
         return self.values[-1]
 
 
+def tf_adam_scalars(lr, t, b1, b2, dtype):
+    """ResourceApplyAdam's scalars in the variables' dtype T, as TF forms them (Keras
+    Adam casts lr, beta_1, beta_2 to T, beta_i_power = pow(beta_i, t) in T; the op computes
+    alpha = lr * sqrt(T(1) - beta2_power) / (T(1) - beta1_power) and T(1) - beta_i in T):
+    (alpha, 1 - b1, 1 - b2) as Python floats holding T values."""
+    f = np.float32 if dtype == torch.float32 else np.float64
+    one, b1t, b2t = f(1), f(b1), f(b2)
+    b1p, b2p = np.power(b1t, f(t)), np.power(b2t, f(t))
+    alpha = f(lr) * np.sqrt(one - b2p) / (one - b1p)
+    return float(alpha), float(one - b1t), float(one - b2t)
+
+
 class TFAdam:
     """Adam with TensorFlow's update (ResourceApplyAdam):
         alpha = lr * sqrt(1 - b2^t) / (1 - b1^t)
         m += (g - m)(1 - b1);  v += (g^2 - v)(1 - b2);  var -= m*alpha / (sqrt(v) + eps)
+    every scalar formed in the variables' dtype (tf_adam_scalars);
     lr = schedule(iterations) before the increment, t = iterations + 1.  None
     gradients are skipped (Keras filters them), iterations still advance."""
 
@@ -258,7 +271,6 @@ class TFAdam:
         applied in parts (disjoint variable sets, same lr and t)."""
         lr = self.schedule(self.iterations)
         t = self.iterations + 1
-        alpha = lr * np.sqrt(1 - self.b2 ** t) / (1 - self.b1 ** t)
         gs, vs, ms, ss = [], [], [], []
         for g, v in grads_and_vars:
             if g is None:
@@ -267,13 +279,15 @@ class TFAdam:
             if st is None:
                 st = self.state[v] = (torch.zeros_like(v), torch.zeros_like(v))
             gs.append(g); vs.append(v); ms.append(st[0]); ss.append(st[1])
+        if gs:
+            alpha, omb1, omb2 = tf_adam_scalars(lr, t, self.b1, self.b2, vs[0].dtype)
         if gs and gs[0].is_cuda:  # one dpac_adam_apply launch (same arithmetic, same order)
             ops.adam_apply([v.data for v in vs], [g.detach().contiguous() for g in gs], ms, ss, alpha,
                            self.b1, self.b2, self.eps)
         elif gs:
-            torch._foreach_add_(ms, torch._foreach_mul(torch._foreach_sub(gs, ms), 1 - self.b1))
+            torch._foreach_add_(ms, torch._foreach_mul(torch._foreach_sub(gs, ms), omb1))
             g2 = torch._foreach_mul(gs, gs)
-            torch._foreach_add_(ss, torch._foreach_mul(torch._foreach_sub(g2, ss), 1 - self.b2))
+            torch._foreach_add_(ss, torch._foreach_mul(torch._foreach_sub(g2, ss), omb2))
             den = torch._foreach_add(torch._foreach_sqrt(ss), self.eps)
             torch._foreach_sub_(vs, torch._foreach_div(torch._foreach_mul(ms, alpha), den))
         if advance:
@@ -402,10 +416,13 @@ class ActorCriticSolver(object):
     """solver.py:7-136.
 
     Extra keyword arguments (all optional; defaults reproduce the reference):
-      seed     -- seeds the weight initialisers and the samplers (the reference
-                  is unseeded, SURVEY.md quirk 2);
+      seed     -- seeds the weight initialisers and the device sampler (the
+                  reference is unseeded); with data parallelism
+                  rank 0's seed is used on every rank, drawn or given;
       sampler  -- "device" (rocRAND Philox on the GPU, default) or "host" (the
-                  reference's numpy/scipy stream, bit-identical inputs);
+                  reference's numpy/scipy stream on numpy's global RandomState,
+                  bit-identical inputs: seed it with np.random.seed, as the
+                  reference would be);
       parallel -- a parallel.DataParallel for multi-GPU data parallelism;
       graphs   -- capture each training step's gradient evaluation as a HIP graph
                   (default: on with the device sampler; results are identical).
@@ -424,7 +441,9 @@ class ActorCriticSolver(object):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         _lib.load()
         self.par = parallel or SingleProcess()
-        self.seed = int(seed if seed is not None else np.random.randint(0, 2 ** 31 - 1))
+        # one seed for every rank: the Philox stream is keyed by global trajectory index,
+        # so the shards of a batch are its rows whatever the world size
+        self.seed = self.par.broadcast_int(seed if seed is not None else np.random.randint(0, 2 ** 31 - 1))
         self.sampler = sampler or self.train_config.get("sampler", "device")
         if self.sampler not in ("device", "host"):
             raise ValueError("sampler must be 'device' or 'host'")
@@ -461,8 +480,6 @@ class ActorCriticSolver(object):
         self._graphs = {}
         self._side = None
         self._side_g = None
-        if self.sampler == "host":
-            self._np_rng_state = None
 
     # ---- variables ---------------------------------------------------------
     def critic_variables(self):
@@ -794,14 +811,15 @@ class ActorCriticSolver(object):
                             step, loss_critic, loss_actor, err_value, err_value_infty, err_control,
                             err_value_grad, err_cost, elapsed_time))
             if step == nc.num_iterations:
-                with torch.no_grad():
+                with torch.no_grad():  # solver.py:63-66 on the whole validation set
                     xv = valid_data_critic.x0
-                    x0 = xv.cpu().numpy()
-                    y = self.model_critic.NN_value(xv).cpu().numpy()
-                    true_y = self.bsde.V_true(xv).cpu().numpy()
-                    grad_y = self.model_critic.NN_value_grad(xv).cpu().numpy()
-                    z = self.model_actor.NN_control(xv).cpu().numpy()
-                    true_z = self.bsde.u_true(xv).cpu().numpy()
+                    g = lambda t: self.par.gather_rows(t, V).cpu().numpy()  # global row order
+                    x0 = g(xv)
+                    y = g(self.model_critic.NN_value(xv))
+                    true_y = g(self.bsde.V_true(xv))
+                    grad_y = g(self.model_critic.NN_value_grad(xv))
+                    z = g(self.model_actor.NN_control(xv))
+                    true_z = g(self.bsde.u_true(xv))
                 if self.par.rank == 0:
                     print("true loss actor: ", true_loss_actor)
                 training_history.append([0, 0.0, true_loss_actor, 0.0, 0.0, 0.0, 0.0, 0.0, elapsed_time])

@@ -229,11 +229,11 @@ int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
  *   weight[i] = [width[i]][width[i+1]] row-major (x @ W), i = 0..n_hidden;
  *   bias = [out];
  *   weight_km[i] (optional, float only; NULL = not used): the k-major image of
- *     the i-th product's right operand, [cols][K16] with K16 = roundup(K, 16) and
- *     zeros for k >= K.  For dpac_rollout_nn_fwd the operand is weight[i]
- *     (K = width[i], cols = width[i+1]), as for dpac_mlp_rows_fwd; for
- *     dpac_rollout_nn_bwd and dpac_mlp_rows_bwd it is weight_t[i] (K = width[i+1],
- *     cols = width[i]).  dpac_mlp_prepare writes both.
+ *     weight[i], [cols][K16] with K = width[i], cols = width[i+1], K16 =
+ *     roundup(K, 16) and zeros for k >= K, read by the FORWARD entry points
+ *     (dpac_rollout_nn_fwd, dpac_mlp_rows_fwd).  The backward entry points ignore
+ *     it and take the images of weight_t in their own `weight_t_km` argument, so
+ *     one struct serves both directions.  dpac_mlp_prepare writes both kinds.
  *     The wide layers then load 4 k per lane and instruction.
  * 1 <= n_hidden <= DPAC_MLP_MAX_HIDDEN, every width <= DPAC_MLP_MAX_WIDTH.
  * Outputs as dpac_rollout_fwd, with u [N][B][c] the control actually applied.
@@ -265,7 +265,9 @@ int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
 /* The actor's BPTT through a dpac_rollout_nn_fwd rollout (what GradientTape does
  * for solver.py:92-97), as one launch.  Inputs: the forward's x, u, dw and its
  * saves; `weight_t[i]` = (weight[i] * bn_scale[i+1])^T, [width[i+1]][width[i]]
- * row-major, i = 0..n_hidden; the upstream gradients g_xN [B][d] (dL/dx_N),
+ * row-major, i = 0..n_hidden; weight_t_km (optional, float only, NULL = not used)
+ * their k-major images, [width[i]][roundup(width[i+1], 16)] (dpac_mlp_prepare's
+ * weight_t_km output); the upstream gradients g_xN [B][d] (dL/dx_N),
  * g_disc [B] (dL/d disc_N) and g_y [B] (dL/dy, the actor-order cost), each
  * optional (NULL = 0).  Output G [N][B][Σ_i width[i]]: block i (column offset
  * Σ_{k<i} width[k]) is dL/d(output of BN_i) at step t — for i = 0 the gradient
@@ -274,7 +276,8 @@ int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
  * products over the N*B rows.  g_x0 [B][d] (optional): dL/dx_0. */
 int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
                         int64_t num_sample, int32_t num_steps, double total_time,
-                        const dpac_mlp* actor, const void* const* weight_t, const void* x,
+                        const dpac_mlp* actor, const void* const* weight_t,
+                        const void* const* weight_t_km, const void* x,
                         const void* u, const void* dw, const void* save_z,
                         const int32_t* save_flag, const void* save_disc, const void* g_xN,
                         const void* g_disc, const void* g_y, void* G, void* g_x0, void* stream);
@@ -290,11 +293,13 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
  * Backward: given g_out [rows][width[n_hidden+1]] (dL/d out) and the forward's
  * save_z, writes G [rows][Σ_i width[i]], block i = dL/d(output of BN_i) — the
  * input of dpac_mlp_param_grads — and optionally g_x [rows][width[0]] = dL/dx.
- * weight_t[i] = (weight[i] * bn_scale[i+1])^T, [width[i+1]][width[i]] row-major. */
+ * weight_t[i] = (weight[i] * bn_scale[i+1])^T, [width[i+1]][width[i]] row-major;
+ * weight_t_km (optional, float only) their k-major images, as for dpac_rollout_nn_bwd. */
 int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* x,
                       int64_t ldx, void* out, void* save_z, void* stream);
 int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* const* weight_t,
-                      const void* save_z, const void* g_out, void* G, void* g_x, void* stream);
+                      const void* const* weight_t_km, const void* save_z, const void* g_out, void* G,
+                      void* g_x, void* stream);
 
 /* ---- parameter gradients of a dpac_mlp over independent rows -------------
  * What GradientTape returns for DeepNN's trainable variables (solver.py:88,95

@@ -1,7 +1,7 @@
 """ORACLE (test infrastructure only): restatement of equation.py on torch-CPU / numpy.
 
 Every TF op of the reference is replaced by the torch op with the same meaning,
-in the same order, on float64 tensors; gradients come from torch autograd (the
+in the same order, on float64 tensors (oracle.precision; float32 only for bench.py's CPU timing); gradients come from torch autograd (the
 analogue of tf.GradientTape).  Tensor layouts are the reference's: x [B, d],
 dw [B, d, N], x_smp [B, d, N+1], dt / coef [B, N].
 """
@@ -9,11 +9,13 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+
+from .precision import dtype as _dt
 from scipy.stats import multivariate_normal as normal
 
 
 def _t(a):
-    return a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a), dtype=torch.float64)
+    return a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a), dtype=_dt())
 
 
 class Equation:
@@ -68,7 +70,7 @@ class Equation:
         xs = [x0]
         coefs = []
         x_i = x0
-        flag = torch.ones(num_sample, dtype=torch.float64)
+        flag = torch.ones(num_sample, dtype=_dt())
         for i in range(N):
             u_i = self.u_true(x_i) if cheat else NN_control(x_i, training, need_grad=False)
             delta_x = (self.drift(x_i, u_i) * delta_t
@@ -81,7 +83,7 @@ class Equation:
             x_i = x_i + delta_x * coef_i.reshape(num_sample, 1)
             xs.append(x_i)
             flag = flag * (1 - Exit)
-        dt = torch.ones(num_sample, N, dtype=torch.float64) * delta_t
+        dt = torch.ones(num_sample, N, dtype=_dt()) * delta_t
         return torch.stack(xs, 2), dt, torch.stack(coefs, 1)
 
     def propagate_adaptive(self, num_sample, x0, dw_sample, NN_control, training, T, N, cheat):
@@ -93,7 +95,7 @@ class Equation:
         x0_norm = torch.sqrt(torch.sum(x0 ** 2, 1))
         layer = self.sigma_Up * np.sqrt(3 * self.dim * delta_t)
         temp = torch.sign(self.R - x0_norm - layer) + torch.sign(self.R - x0_norm)
-        flag = torch.ones(num_sample, dtype=torch.float64) + torch.floor(temp / 2)
+        flag = torch.ones(num_sample, dtype=_dt()) + torch.floor(temp / 2)
         for i in range(N):
             xi_norm = torch.sqrt(torch.sum(x_i ** 2, 1))
             dt_i = ((2 * flag - (flag ** 2)) * ((self.R - xi_norm) ** 2)
@@ -108,7 +110,7 @@ class Equation:
             x_next = x_i + delta_x
             x_next_norm = torch.sqrt(torch.sum(x_next ** 2, 1))
             temp = torch.sign(self.R - x_next_norm - layer) + torch.sign(self.R - x_next_norm)
-            new_flag = (torch.ones(num_sample, dtype=torch.float64) + torch.floor(temp / 2)) * torch.sign(flag)
+            new_flag = (torch.ones(num_sample, dtype=_dt()) + torch.floor(temp / 2)) * torch.sign(flag)
             coef_i = torch.sign(flag) * torch.sign(new_flag)
             coefs.append(coef_i)
             dts.append(dt_i)
@@ -156,7 +158,7 @@ class LQR(Equation):
         return 2 * self.k * x
 
     def sigma(self, x, u, num_sample):
-        return np.sqrt(2.0) * torch.ones(num_sample, 1, 1, dtype=torch.float64) * torch.eye(self.dim, dtype=torch.float64)
+        return np.sqrt(2.0) * torch.ones(num_sample, 1, 1, dtype=_dt()) * torch.eye(self.dim, dtype=_dt())
 
     def drift(self, x, u):
         return self.beta * u
@@ -208,7 +210,7 @@ class VDP(Equation):
                           2 * self.a * x2 - self.epsl * (px2 + nx2)], 1)
 
     def sigma(self, x, u, num_sample):
-        return np.sqrt(2.0) * torch.ones(num_sample, 1, 1, dtype=torch.float64) * torch.eye(self.dim, dtype=torch.float64)
+        return np.sqrt(2.0) * torch.ones(num_sample, 1, 1, dtype=_dt()) * torch.eye(self.dim, dtype=_dt())
 
     def drift(self, x, u):
         x_1 = x[:, 0:self.control_dim]
@@ -245,7 +247,7 @@ class ekn(Equation):
         return (3 * self.a3 * x_norm - 2 * self.a2) * x
 
     def sigma(self, x, u, num_sample):
-        return np.sqrt(2.0) * torch.ones(num_sample, 1, 1, dtype=torch.float64) * torch.eye(self.dim, dtype=torch.float64)
+        return np.sqrt(2.0) * torch.ones(num_sample, 1, 1, dtype=_dt()) * torch.eye(self.dim, dtype=_dt())
 
     def drift(self, x, u):
         x_norm = torch.sum(x ** 2, 1, keepdim=True) ** 0.5

@@ -13,6 +13,8 @@ import time
 import numpy as np
 import torch
 
+from .precision import dtype as _dt
+
 DELTA_CLIP = 50.0  # solver.py:5
 BN_EPS = 1e-6      # solver.py:242
 
@@ -40,7 +42,7 @@ class DeepNN:
     def __call__(self, x, training=False, need_grad=False):
         p = self.params
         L = len(self.sizes) - 2
-        inv = lambda i: torch.rsqrt(torch.tensor(1.0 + BN_EPS, dtype=torch.float64)) * p["bn_gamma"][i]
+        inv = lambda i: torch.rsqrt(torch.tensor(1.0 + BN_EPS, dtype=_dt())) * p["bn_gamma"][i]
         y = x * inv(0) + p["bn_beta"][0]
         for i in range(L):
             y = y @ p["W"][i]
@@ -62,13 +64,13 @@ def init_params(sizes, gen: torch.Generator):
     """Keras initialisers: BN gamma U(0.1,0.5), beta N(0,0.1); Dense glorot_uniform; bias 0."""
     L = len(sizes) - 2
     bn_dims = [sizes[0]] + list(sizes[1:-1]) + [sizes[-1]]
-    g = [torch.rand(n, generator=gen, dtype=torch.float64) * 0.4 + 0.1 for n in bn_dims]
-    b = [torch.randn(n, generator=gen, dtype=torch.float64) * 0.1 for n in bn_dims]
+    g = [torch.rand(n, generator=gen, dtype=_dt()) * 0.4 + 0.1 for n in bn_dims]
+    b = [torch.randn(n, generator=gen, dtype=_dt()) * 0.1 for n in bn_dims]
     W = []
     for i in range(L + 1):
         lim = np.sqrt(6.0 / (sizes[i] + sizes[i + 1]))
-        W.append((torch.rand(sizes[i], sizes[i + 1], generator=gen, dtype=torch.float64) * 2 - 1) * lim)
-    return {"bn_gamma": g, "bn_beta": b, "W": W, "b": torch.zeros(sizes[-1], dtype=torch.float64)}
+        W.append((torch.rand(sizes[i], sizes[i + 1], generator=gen, dtype=_dt()) * 2 - 1) * lim)
+    return {"bn_gamma": g, "bn_beta": b, "W": W, "b": torch.zeros(sizes[-1], dtype=_dt())}
 
 
 class CriticModel:
@@ -89,7 +91,7 @@ class CriticModel:
         return self.bsde.u_true(x)
 
     def __call__(self, inputs, model_actor, training, cheat_control):
-        x0, dw, x_bdry = [torch.as_tensor(np.asarray(a), dtype=torch.float64) if not isinstance(a, torch.Tensor) else a
+        x0, dw, x_bdry = [torch.as_tensor(np.asarray(a), dtype=_dt()) if not isinstance(a, torch.Tensor) else a
                           for a in inputs]
         num_sample = dw.shape[0]
         y = 0
@@ -126,7 +128,7 @@ class ActorModel:
         self.propagate = bsde.propagate_naive if config.train_config.scheme == "naive" else bsde.propagate_adaptive
 
     def __call__(self, inputs, model_critic, training, cheat_value, cheat_control):
-        x0, dw, x_bdry = [torch.as_tensor(np.asarray(a), dtype=torch.float64) if not isinstance(a, torch.Tensor) else a
+        x0, dw, x_bdry = [torch.as_tensor(np.asarray(a), dtype=_dt()) if not isinstance(a, torch.Tensor) else a
                           for a in inputs]
         num_sample = dw.shape[0]
         y = 0
@@ -245,30 +247,30 @@ class ActorCriticSolver:
         self.optimizer_actor.apply_gradients(zip(g, self.actor_vars()))
 
     def err_value(self, inputs):
-        x0 = torch.as_tensor(inputs[0], dtype=torch.float64)
+        x0 = torch.as_tensor(inputs[0], dtype=_dt())
         with torch.no_grad():
             e = torch.sum(torch.square(self.bsde.V_true(x0) - self.model_critic.NN_value(x0)))
             return torch.sqrt(e / torch.sum(torch.square(self.bsde.V_true(x0))))
 
     def err_control(self, inputs):
-        x0 = torch.as_tensor(inputs[0], dtype=torch.float64)
+        x0 = torch.as_tensor(inputs[0], dtype=_dt())
         with torch.no_grad():
             e = torch.sum(torch.square(self.bsde.u_true(x0) - self.model_actor.NN_control(x0)))
             return torch.sqrt(e / torch.sum(torch.square(self.bsde.u_true(x0))))
 
     def err_value_grad(self, inputs):
-        x0 = torch.as_tensor(inputs[0], dtype=torch.float64)
+        x0 = torch.as_tensor(inputs[0], dtype=_dt())
         with torch.no_grad():
             e = torch.sum(torch.square(self.bsde.V_grad_true(x0) - self.model_critic.NN_value_grad(x0)))
             return torch.sqrt(e / torch.sum(torch.square(self.bsde.V_grad_true(x0))))
 
     def err_value_infty(self, inputs):
-        x0 = torch.as_tensor(inputs[0], dtype=torch.float64)
+        x0 = torch.as_tensor(inputs[0], dtype=_dt())
         with torch.no_grad():
             return torch.max(torch.abs(self.bsde.V_true(x0) - self.model_critic.NN_value(x0)))
 
     def err_cost(self, inputs):
-        x0 = torch.as_tensor(inputs[0], dtype=torch.float64)
+        x0 = torch.as_tensor(inputs[0], dtype=_dt())
         with torch.no_grad():
             y = self.model_actor(inputs, self.model_critic, False, False, False)
             return torch.mean(y - self.model_critic.NN_value(x0))

@@ -239,12 +239,13 @@ def test_adam_kernel_matches_foreach_update(dtype):
     m_dev = [torch.zeros_like(v) for v in dev]
     s_dev = [torch.zeros_like(v) for v in dev]
     b1, b2, eps = 0.9, 0.999, 1e-8
+    from deeppde_actorcritic_amd.solver import tf_adam_scalars
     for t in range(1, 4):
         gs = [torch.randn(s, generator=gen, dtype=dtype).cuda() for s in shapes]
-        alpha = 1e-3 * np.sqrt(1 - b2 ** t) / (1 - b1 ** t)
-        torch._foreach_add_(m_ref, torch._foreach_mul(torch._foreach_sub(gs, m_ref), 1 - b1))
+        alpha, omb1, omb2 = tf_adam_scalars(1e-3, t, b1, b2, dtype)  # TF forms them in T
+        torch._foreach_add_(m_ref, torch._foreach_mul(torch._foreach_sub(gs, m_ref), omb1))
         g2 = torch._foreach_mul(gs, gs)
-        torch._foreach_add_(s_ref, torch._foreach_mul(torch._foreach_sub(g2, s_ref), 1 - b2))
+        torch._foreach_add_(s_ref, torch._foreach_mul(torch._foreach_sub(g2, s_ref), omb2))
         den = torch._foreach_add(torch._foreach_sqrt(s_ref), eps)
         torch._foreach_sub_(ref, torch._foreach_div(torch._foreach_mul(m_ref, alpha), den))
         ops.adam_apply(dev, gs, m_dev, s_dev, alpha, b1, b2, eps)

@@ -1,0 +1,77 @@
+"""GPU: training (solver.py:36-71) at d = 20 against the float64 oracle.
+
+* Joint actor-critic training of every BASELINE equation at d = 20 (VDP with c = 10) against
+  the live oracle, small nets, both the eager path and the production path (HIP graphs, the
+  critic step split at the G network, the actor's forward rollout on a side stream).
+* lqr_d20 at BASELINE's batch (B = 4096, N = 100, 3x200 MLPs, TD1, adaptive) against the
+  committed oracle vectors tests/golden/train_lqr_d20_B4096.npz (made by
+  tests/golden/make_train_golden.py; the oracle needs about a CPU-minute per iteration there).
+Same initial weights (ActorCriticSolver(seed) draws the Keras initialisers from
+torch.Generator().manual_seed(seed), which the oracle's init_params reproduces) and the same
+numpy sample stream (sampler="host").  Tolerance: 1e-8 relative (float64; GEMM and reduction
+re-association only).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from deeppde_actorcritic_amd import equation as peq
+from deeppde_actorcritic_amd import solver as psol
+from oracle import equations as oeq
+from oracle import solver as osol
+from tests.helpers import full_config, rel_close
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_lqr_d20_B4096.npz")
+
+
+def pair(cfg, seed, graphs):
+    bp = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
+    sp = psol.ActorCriticSolver(cfg, bp, seed=seed, sampler="host", graphs=graphs)
+    params = {"critic": sp.model_critic.NN_value.export_params(),
+              "critic_grad": sp.model_critic.NN_value_grad.export_params(),
+              "actor": sp.model_actor.NN_control.export_params()}
+    return sp, osol.ActorCriticSolver(cfg, oeq.make(cfg.eqn_config), params=params)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+@pytest.mark.parametrize("name", ["VDP", "LQR", "EKN", "LQR_var"])
+def test_joint_training_d20_matches_oracle(name, graphs):
+    cfg = full_config(name, 20, N=10, hidden=(32, 32), batch=48, valid=48, iters=3, log_freq=1,
+                      train="actor-critic", td="TD1")
+    sp, so = pair(cfg, 13, graphs)
+    np.random.seed(77)
+    hp = sp.train()
+    np.random.seed(77)
+    ho = so.train()
+    assert hp[0].shape == ho.shape == (5, 9)
+    assert rel_close(hp[0][:, 1:8], ho[:, 1:8], 1e-8)
+    for vp, vo in zip(sp.critic_variables() + sp.actor_variables(), so.critic_vars() + so.actor_vars()):
+        assert rel_close(vp.detach().cpu(), vo.detach(), 1e-8)
+
+
+def summarize(tensors):
+    out = []
+    for t in tensors:
+        t = t.detach().to("cpu", torch.float64).reshape(-1)
+        out.append([float(t.sum()), float((t * t).sum())] + t[:16].tolist() + [0.0] * (16 - min(16, t.numel())))
+    return np.array(out, dtype=np.float64)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_lqr_d20_baseline_batch_matches_oracle_vectors(graphs):
+    from deeppde_actorcritic_amd.config import baseline_config
+    g = np.load(GOLDEN)
+    seed_params, seed_np, iters, batch, valid = (int(v) for v in g["meta"])
+    cfg = baseline_config(iters, 1, "float64", batch, valid, "lqr_d20")
+    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=seed_params, sampler="host", graphs=graphs)
+    np.random.seed(seed_np)
+    hist = sp.train()[0]
+    ref = g["history"]
+    assert hist.shape == ref.shape
+    assert rel_close(hist[:, 1:8], ref[:, 1:8], 1e-8)
+    got = summarize(sp.critic_variables() + sp.actor_variables())
+    assert got.shape == g["params"].shape
+    assert rel_close(got, g["params"], 1e-8)

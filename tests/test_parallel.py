@@ -105,3 +105,37 @@ def test_gloo_world2_gradients_equal_full_batch():
         err = eq.V_true(x0t) - so.model_critic.NN_value(x0t)
     assert abs(res["num"] - float(torch.sum(err ** 2))) < 1e-12 * (1 + float(torch.sum(err ** 2)))
     assert res["max"] == float(torch.max(torch.abs(err)))
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        par = DataParallel()
+        total = 11  # ragged: shards of 4, 4, 3
+        off, cnt = par.shard(total)
+        rows = torch.arange(total * 3, dtype=torch.float64).view(total, 3)[off:off + cnt]
+        got = par.gather_rows(rows, total)
+        seed = par.broadcast_int(1000 + rank)  # every rank ends up with rank 0's value
+        q.put((rank, got, seed))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world3_gather_rows_and_seed_broadcast():
+    """parallel.DataParallel.gather_rows (train()'s final validation arrays, solver.py:63-66,
+    in global row order from ragged shards) and broadcast_int (one seed on every rank)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(3)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = torch.arange(33, dtype=torch.float64).view(11, 3)
+    for rank, got, seed in res:
+        assert torch.equal(got, full)
+        assert seed == 1000

@@ -65,11 +65,10 @@ def main():
         widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
         view, wt, wt_km = ops.mlp_prepare([p.detach() for p in gam], [p.detach() for p in bet],
                                           [p.detach() for p in Ws], b.detach(), False, True)
-        bview = view if wt_km is None else view.with_km(wt_km)
         g_y = torch.full_like(y, 1.0 / B)
         g_disc = torch.rand_like(y) / B
         g_xN = torch.randn_like(xN) / B
-        bwd = lambda: ops._bptt_fused(eqp, sch, 0.2, N, L, x, u, dwc, z, flag, disc_t, bview, wt, widths,
+        bwd = lambda: ops._bptt_fused(eqp, sch, 0.2, N, L, x, u, dwc, z, flag, disc_t, view, wt, wt_km, widths,
                                       g_xN, g_disc, g_y)
         G = bwd()
         Gall = ops.G_all(G)

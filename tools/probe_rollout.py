@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--scheme", default="adaptive")
     ap.add_argument("--philox", action="store_true")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--sets", type=int, default=1, help="rotate over this many buffer sets (5: not MALL-resident)")
     a = ap.parse_args()
     from deeppde_actorcritic_amd import _lib, ops
     from deeppde_actorcritic_amd import equation as peq
@@ -36,28 +37,32 @@ def main():
         cfg = eqn_config(a.eqn, a.d, T=0.2, N=N)
         eqp = getattr(peq, a.eqn)(cfg).params()
         for B in [int(v) for v in a.B.split(",")]:
-            x0, dw, _ = ops.sample(eqp, 0, B, N, seed=1, dtype=dt_, device="cuda")
-            x = torch.empty(N + 1, B, a.d, dtype=dt_, device="cuda")
-            dt = torch.empty(B, N, dtype=dt_, device="cuda")
-            coef = torch.empty(B, N, dtype=dt_, device="cuda")
             P = ctypes.c_void_p
-            args = (ctypes.byref(eqp), sch, _lib.F32 if dt_ == torch.float32 else _lib.F64, B, N, 0.2,
-                    P(x0.data_ptr()), None if a.philox else P(dw.data_ptr()), 1, 0, 0, P(x.data_ptr()),
-                    P(dt.data_ptr()), P(coef.data_ptr()), None, 0, None, None,
-                    P(torch.cuda.current_stream().cuda_stream))
+            keep, argl = [], []
+            for k in range(a.sets):
+                x0, dw, _ = ops.sample(eqp, 0, B, N, seed=1 + k, dtype=dt_, device="cuda")
+                x = torch.empty(N + 1, B, a.d, dtype=dt_, device="cuda")
+                dt = torch.empty(B, N, dtype=dt_, device="cuda")
+                coef = torch.empty(B, N, dtype=dt_, device="cuda")
+                keep.append((x0, dw, x, dt, coef))
+                argl.append((ctypes.byref(eqp), sch, _lib.F32 if dt_ == torch.float32 else _lib.F64, B, N, 0.2,
+                             P(x0.data_ptr()), None if a.philox else P(dw.data_ptr()), 1, 0, 0, P(x.data_ptr()),
+                             P(dt.data_ptr()), P(coef.data_ptr()), None, 0, None, None,
+                             P(torch.cuda.current_stream().cuda_stream)))
+            args = argl[0]
             for _ in range(5):
                 lib.dpac_rollout_fwd(*args)
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            for _ in range(a.reps):
-                assert lib.dpac_rollout_fwd(*args) == 0
+            for i in range(a.reps):
+                assert lib.dpac_rollout_fwd(*argl[i % a.sets]) == 0
             e.record()
             torch.cuda.synchronize()
             ms = s.elapsed_time(e) / a.reps
             esz = 4 if dt_ == torch.float32 else 8
             byts = B * N * ((a.d if not a.philox else 0) + a.d + 2) * esz
-            print(json.dumps({"B": B, "N": N, "d": a.d, "eqn": a.eqn, "dtype": a.dtype, "philox": a.philox,
+            print(json.dumps({"B": B, "N": N, "d": a.d, "eqn": a.eqn, "dtype": a.dtype, "philox": a.philox, "sets": a.sets,
                               "us": ms * 1e3, "ns_per_step": ms * 1e6 / N, "GBps": byts / ms / 1e6,
                               "traj_steps_per_s": B * N / ms * 1e3}), flush=True)
 
