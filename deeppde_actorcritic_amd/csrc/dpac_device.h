@@ -57,23 +57,23 @@ struct Own {
   static constexpr int M = (D + P - 1) / P;
   static constexpr bool kFull = (D % M) == 0;  // every lane is either full or empty
   int p;
-  __device__ explicit Own(int p_) : p(p_) {}
-  __device__ int j(int m) const { return p * M + m; }
-  __device__ bool valid(int m) const { return p * M + m < D; }
-  __device__ bool active() const { return p * M < D; }
+  __device__ __forceinline__ explicit Own(int p_) : p(p_) {}
+  __device__ __forceinline__ int j(int m) const { return p * M + m; }
+  __device__ __forceinline__ bool valid(int m) const { return p * M + m < D; }
+  __device__ __forceinline__ bool active() const { return p * M < D; }
   template <typename T>
-  __device__ void mask(T (&v)[M]) const {
+  __device__ __forceinline__ void mask(T (&v)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) v[m] = valid(m) ? v[m] : T(0);
   }
   // plain-pointer forms (predicated) for the single-step kernels
   template <typename T>
-  __device__ void load_masked(const T* __restrict__ row, T (&v)[M]) const {
+  __device__ __forceinline__ void load_masked(const T* __restrict__ row, T (&v)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) v[m] = valid(m) ? row[p * M + m] : T(0);
   }
   template <typename T>
-  __device__ void store(T* __restrict__ row, const T (&v)[M]) const {
+  __device__ __forceinline__ void store(T* __restrict__ row, const T (&v)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m)
       if (valid(m)) row[p * M + m] = v[m];
@@ -154,7 +154,7 @@ struct BufSlab {
   static constexpr bool kVec = Own<D, P>::kFull;
   static constexpr int K = M * (int)sizeof(T) / 4;
   uint32_t off[kVec ? 1 : M];
-  __device__ BufSlab(const Own<D, P>& own, int64_t b, bool live) {
+  __device__ __forceinline__ BufSlab(const Own<D, P>& own, int64_t b, bool live) {
     if constexpr (kVec) {
       off[0] = (live && own.active()) ? (uint32_t)((b * D + own.p * M) * (int64_t)sizeof(T)) : kOOB;
     } else {
@@ -165,7 +165,7 @@ struct BufSlab {
   }
   // soff: wave-uniform byte offset of the row block (the step), in soffset.
   template <int AUX = 0>
-  __device__ void load(__amdgpu_buffer_rsrc_t r, T (&v)[M], uint32_t soff = 0) const {
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, T (&v)[M], uint32_t soff = 0) const {
     if constexpr (kVec) {
       uint32_t w[K];
       buf_load_dwords<K, AUX>(r, off[0], w, soff);
@@ -180,7 +180,7 @@ struct BufSlab {
     }
   }
   template <int AUX = 0>
-  __device__ void store(__amdgpu_buffer_rsrc_t r, const T (&v)[M], uint32_t soff = 0) const {
+  __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t r, const T (&v)[M], uint32_t soff = 0) const {
     if constexpr (kVec) {
       uint32_t w[K];
       __builtin_memcpy(&w[0], &v[0], sizeof(w));
@@ -321,7 +321,7 @@ struct Rng;
 template <>
 struct Rng<float> {
   static constexpr int kNormalPerBlock = 4;
-  __device__ static void normals(uint4 v, float (&o)[4]) {
+  __device__ __forceinline__ static void normals(uint4 v, float (&o)[4]) {
     box_muller_hw(v.x, v.y, o[0], o[1]);
     box_muller_hw(v.z, v.w, o[2], o[3]);
   }
@@ -329,7 +329,7 @@ struct Rng<float> {
 template <>
 struct Rng<double> {
   static constexpr int kNormalPerBlock = 2;
-  __device__ static void normals(uint4 v, double (&o)[2]) {
+  __device__ __forceinline__ static void normals(uint4 v, double (&o)[2]) {
     const double2 n = rocrand_device::detail::normal_distribution_double2(v);
     o[0] = n.x;
     o[1] = n.y;
@@ -421,40 +421,40 @@ struct EqLQR {
     r.two_p = (T)(2.0 * e.p); r.two_q = (T)(2.0 * e.q);
     return r;
   }
-  __device__ void u_true(const T (&x)[M], T, T (&u)[MC]) const {
+  __device__ __forceinline__ void u_true(const T (&x)[M], T, T (&u)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) u[m] = kappa * x[m];
   }
-  __device__ void drift(const T (&x)[M], const T (&u)[MC], T, T (&f)[M]) const {
+  __device__ __forceinline__ void drift(const T (&x)[M], const T (&u)[MC], T, T (&f)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) f[m] = beta * u[m];
   }
-  __device__ void sigma(const T (&x)[M], const T (&u)[MC], T (&s)[M]) const {
+  __device__ __forceinline__ void sigma(const T (&x)[M], const T (&u)[MC], T (&s)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) s[m] = sqrt2;
   }
-  __device__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
+  __device__ __forceinline__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
     T a = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) a += p * (x[m] * x[m]) + q * (u[m] * u[m]);
     return a;
   }
-  __device__ T w_finish(T s) const { return s - two_kd; }
-  __device__ T V_true(const T (&x)[M], T S, T r) const { return S * k; }
-  __device__ T Z(const T (&x)[M], T S, T r) const { return kR2; }
-  __device__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
+  __device__ __forceinline__ T w_finish(T s) const { return s - two_kd; }
+  __device__ __forceinline__ T V_true(const T (&x)[M], T S, T r) const { return S * k; }
+  __device__ __forceinline__ T Z(const T (&x)[M], T S, T r) const { return kR2; }
+  __device__ __forceinline__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) g[m] = two_k * x[m];
   }
   // VJPs: accumulate a·∂drift/∂(x,u), a·∂sigma/∂(x,u), gw·∂w/∂(x,u)
-  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
+  __device__ __forceinline__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
                             T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) gu[m] += beta * a[m];
   }
-  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
+  __device__ __forceinline__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
                             T (&gu)[MC]) const {}
-  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
+  __device__ __forceinline__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       gx[m] += gw * (two_p * x[m]);
@@ -488,19 +488,19 @@ struct EqLQRVar {
     r.two_c1q = (T)(2.0 * (e.k * e.k * (bpe * bpe)) * e.q);
     return r;
   }
-  __device__ void u_true(const T (&x)[M], T, T (&u)[MC]) const {
+  __device__ __forceinline__ void u_true(const T (&x)[M], T, T (&u)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) u[m] = (-bpe * x[m]) / (qk + e2 * (x[m] * x[m]));
   }
-  __device__ void drift(const T (&x)[M], const T (&u)[MC], T, T (&f)[M]) const {
+  __device__ __forceinline__ void drift(const T (&x)[M], const T (&u)[MC], T, T (&f)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) f[m] = beta * u[m];
   }
-  __device__ void sigma(const T (&x)[M], const T (&u)[MC], T (&s)[M]) const {
+  __device__ __forceinline__ void sigma(const T (&x)[M], const T (&u)[MC], T (&s)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) s[m] = sqrt2 * (1 + (eps * x[m]) * u[m]);
   }
-  __device__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
+  __device__ __forceinline__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
     T a = 0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -509,19 +509,19 @@ struct EqLQRVar {
     }
     return a;
   }
-  __device__ T w_finish(T s) const { return s - two_kd; }
-  __device__ T V_true(const T (&x)[M], T S, T r) const { return S * k; }
-  __device__ T Z(const T (&x)[M], T S, T r) const { return kR2; }
-  __device__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
+  __device__ __forceinline__ T w_finish(T s) const { return s - two_kd; }
+  __device__ __forceinline__ T V_true(const T (&x)[M], T S, T r) const { return S * k; }
+  __device__ __forceinline__ T Z(const T (&x)[M], T S, T r) const { return kR2; }
+  __device__ __forceinline__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) g[m] = two_k * x[m];
   }
-  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
+  __device__ __forceinline__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
                             T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) gu[m] += beta * a[m];
   }
-  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
+  __device__ __forceinline__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
                             T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -529,7 +529,7 @@ struct EqLQRVar {
       gu[m] += a[m] * (sqrt2_eps * x[m]);
     }
   }
-  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
+  __device__ __forceinline__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const T den = q + c2 * (x[m] * x[m]);
@@ -553,29 +553,29 @@ struct EqEKN {
     r.sqrt2 = (T)1.4142135623730951;
     return r;
   }
-  __device__ void u_true(const T (&x)[M], T r, T (&u)[MC]) const {
+  __device__ __forceinline__ void u_true(const T (&x)[M], T r, T (&u)[MC]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) u[m] = x[m] / r;  // x / |x| (:261)
   }
-  __device__ void drift(const T (&x)[M], const T (&u)[MC], T r, T (&f)[M]) const {
+  __device__ __forceinline__ void drift(const T (&x)[M], const T (&u)[MC], T r, T (&f)[M]) const {
     const T c = K / (two_a2 - three_a3 * r);
 #pragma unroll
     for (int m = 0; m < M; ++m) f[m] = c * u[m];
   }
-  __device__ void sigma(const T (&x)[M], const T (&u)[MC], T (&s)[M]) const {
+  __device__ __forceinline__ void sigma(const T (&x)[M], const T (&u)[MC], T (&s)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) s[m] = sqrt2;
   }
-  __device__ T w_part(const T (&x)[M], const T (&u)[MC]) const { return 0; }
-  __device__ T w_finish(T) const { return 1; }  // 0*sum(x) + 1 (:250)
-  __device__ T V_true(const T (&x)[M], T S, T r) const { return a3 * (r * r * r) - a2 * (r * r); }
-  __device__ T Z(const T (&x)[M], T S, T r) const { return V_true(x, S, r); }
-  __device__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
+  __device__ __forceinline__ T w_part(const T (&x)[M], const T (&u)[MC]) const { return 0; }
+  __device__ __forceinline__ T w_finish(T) const { return 1; }  // 0*sum(x) + 1 (:250)
+  __device__ __forceinline__ T V_true(const T (&x)[M], T S, T r) const { return a3 * (r * r * r) - a2 * (r * r); }
+  __device__ __forceinline__ T Z(const T (&x)[M], T S, T r) const { return V_true(x, S, r); }
+  __device__ __forceinline__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {
     const T c = three_a3 * r - two_a2;
 #pragma unroll
     for (int m = 0; m < M; ++m) g[m] = c * x[m];
   }
-  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
+  __device__ __forceinline__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
                             T (&gx)[M], T (&gu)[MC]) const {
     const T den = two_a2 - three_a3 * r;
     const T c = K / den;
@@ -591,9 +591,9 @@ struct EqEKN {
 #pragma unroll
     for (int m = 0; m < M; ++m) gx[m] += f * x[m];
   }
-  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
+  __device__ __forceinline__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
                             T (&gu)[MC]) const {}
-  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {}
+  __device__ __forceinline__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {}
 };
 
 // VDP — stochastic Van der Pol oscillator, equation.py:179-238.  x = (x1, x2),
@@ -618,20 +618,20 @@ struct EqVDP {
     r.two_q = (T)(2.0 * e.q);
     return r;
   }
-  __device__ static constexpr int nxt(int i) { return (i + 1) % C; }
-  __device__ static constexpr int prv(int i) { return (i + C - 1) % C; }
+  __device__ __forceinline__ static constexpr int nxt(int i) { return (i + 1) % C; }
+  __device__ __forceinline__ static constexpr int prv(int i) { return (i + C - 1) % C; }
   // dv = 2a*v - eps*(px + nx) on one half (:196-197, :217, :227)
-  __device__ void Lop(const T* v, T* o) const {
+  __device__ __forceinline__ void Lop(const T* v, T* o) const {
 #pragma unroll
     for (int i = 0; i < C; ++i) o[i] = two_a * v[i] - eps * (v[nxt(i)] + v[prv(i)]);
   }
-  __device__ void u_true(const T (&x)[M], T, T (&u)[MC]) const {
+  __device__ __forceinline__ void u_true(const T (&x)[M], T, T (&u)[MC]) const {
     T dv2[C];
     Lop(x + C, dv2);
 #pragma unroll
     for (int i = 0; i < C; ++i) u[i] = -dv2[i] / 2 / q;  // (:217)
   }
-  __device__ void drift(const T (&x)[M], const T (&u)[MC], T, T (&f)[M]) const {
+  __device__ __forceinline__ void drift(const T (&x)[M], const T (&u)[MC], T, T (&f)[M]) const {
 #pragma unroll
     for (int i = 0; i < C; ++i) {
       const T x1 = x[i], x2 = x[C + i];
@@ -639,11 +639,11 @@ struct EqVDP {
       f[C + i] = (1 - x1 * x1) * x2 - x1 + u[i];  // (:235)
     }
   }
-  __device__ void sigma(const T (&x)[M], const T (&u)[MC], T (&s)[M]) const {
+  __device__ __forceinline__ void sigma(const T (&x)[M], const T (&u)[MC], T (&s)[M]) const {
 #pragma unroll
     for (int m = 0; m < M; ++m) s[m] = sqrt2;
   }
-  __device__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
+  __device__ __forceinline__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
     T dv1[C], dv2[C];
     Lop(x, dv1);
     Lop(x + C, dv2);
@@ -658,19 +658,19 @@ struct EqVDP {
     }
     return acc;
   }
-  __device__ T w_finish(T s) const { return s - two_ad; }
-  __device__ T V_true(const T (&x)[M], T S, T r) const {  // (:210)
+  __device__ __forceinline__ T w_finish(T s) const { return s - two_ad; }
+  __device__ __forceinline__ T V_true(const T (&x)[M], T S, T r) const {  // (:210)
     T cross = 0;
 #pragma unroll
     for (int i = 0; i < C; ++i) cross += x[i] * x[nxt(i)] + x[C + i] * x[C + nxt(i)];
     return a * S - eps * cross;
   }
-  __device__ T Z(const T (&x)[M], T S, T r) const { return V_true(x, S, r); }
-  __device__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {  // (:227)
+  __device__ __forceinline__ T Z(const T (&x)[M], T S, T r) const { return V_true(x, S, r); }
+  __device__ __forceinline__ void V_grad(const T (&x)[M], T S, T r, T (&g)[M]) const {  // (:227)
     Lop(x, g);
     Lop(x + C, g + C);
   }
-  __device__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
+  __device__ __forceinline__ void drift_vjp(const T (&x)[M], const T (&u)[MC], T r, const T (&a)[M],
                             T (&gx)[M], T (&gu)[MC]) const {
 #pragma unroll
     for (int i = 0; i < C; ++i) {
@@ -680,13 +680,13 @@ struct EqVDP {
       gu[i] += a2v;
     }
   }
-  __device__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
+  __device__ __forceinline__ void sigma_vjp(const T (&x)[M], const T (&u)[MC], const T (&a)[M], T (&gx)[M],
                             T (&gu)[MC]) const {}
   // gradient of w (derivation in DESIGN.md §4.3): with L v = 2a v - eps(px v + nx v),
   // g = (1 - x1^2) x2 - x1:
   //   dw/dx1 = -gamma*eps*(px1+nx1) + 2 x1 x2 dv2 + 2 gamma a x1
   //   dw/dx2 = -gamma*eps*(px2+nx2) + L(dv2)/(2q) - dv1 - (1 - x1^2) dv2 - L(g) + 2 gamma a x2
-  __device__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
+  __device__ __forceinline__ void w_vjp(const T (&x)[M], const T (&u)[MC], T gw, T (&gx)[M], T (&gu)[MC]) const {
     T dv1[C], dv2[C], g[C], Ldv2[C], Lg[C];
     Lop(x, dv1);
     Lop(x + C, dv2);

@@ -214,7 +214,7 @@ struct LaneCoord {
   int p;
   int64_t b;
   bool live;
-  __device__ LaneCoord(int64_t B, int lane, int64_t group0) {
+  __device__ __forceinline__ LaneCoord(int64_t B, int lane, int64_t group0) {
     p = lane % P;
     b = group0 + lane / P;
     live = b < B;
@@ -226,8 +226,8 @@ struct LaneCoord {
 // layer = flag == 1 (equation.py:80-82: flag 2 inner, 1 boundary layer, 0 out).
 struct Flags {
   bool alive, layer;
-  __device__ int encode() const { return alive ? (layer ? 1 : 2) : 0; }
-  __device__ static Flags decode(int f) { return Flags{f > 0, f == 1}; }
+  __device__ __forceinline__ int encode() const { return alive ? (layer ? 1 : 2) : 0; }
+  __device__ __forceinline__ static Flags decode(int f) { return Flags{f > 0, f == 1}; }
 };
 
 // Region of a point at radius r: 1 + floor((sign(R-r-c) + sign(R-r))/2) is
@@ -772,6 +772,7 @@ __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, i
 }
 
 #include "dpac_rollout_nn.h"
+#include "dpac_rollout_nn_bwd.h"
 #include "dpac_rollout_nn4.h"
 
 // ---------------------------------------------------------------------------
@@ -803,6 +804,12 @@ NnMlp<T> nn_mlp(const dpac_mlp& h) {
 // Row tile of the fused NN rollout for float: 4 (4x4x1 MFMA blocks) or 16
 // (16x16x4 tiles; float64 always uses these); by default 4 for B <= 1024.
 // DPAC_NN_TILE=4 / 16 forces one (tests compare the two).
+// BPTT kernel: 2 = k_rollout_nn_bwd2 (stager + writer wavefronts, default), 1 = k_rollout_nn_bwd.
+inline int bptt_kernel() {
+  const char* e = getenv("DPAC_BPTT");  // read per launch: tests switch it in-process
+  return (e && e[0] == '1') ? 1 : 2;
+}
+
 inline int nn_tile_rows() {
   const char* e = getenv("DPAC_NN_TILE");  // read per launch: tests switch it in-process
   const int v = e ? atoi(e) : 0;
@@ -923,6 +930,27 @@ int run_op(const OpArgs& a) {
         r.wtkm[i] = (const T*)a.mlp.weight_km[i];  // k-major images of wt (dpac.h)
       }
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
+      if (bptt_kernel() == 2) {
+        int wsum = 0;
+        for (int i = 0; i <= m.L + 1; ++i) wsum += m.width[i];
+        const BwdPlan<T, D, E::CDIM> pl(wsum, m.ztot, true);
+        const dim3 nb2(kNnBwdThreads);
+#define DPAC_BWD2(SCH, ZS)                                                                          \
+  {                                                                                                 \
+    auto kfn = k_rollout_nn_bwd2<T, E, D, SCH, ZS>;                                                 \
+    if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                      \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.total)) \
+      return (int)e;                                                                                \
+    hipLaunchKernelGGL(kfn, ngrid, nb2, pl.total, s, eq, c, m, r);                                  \
+  }
+        if (adaptive) {
+          if (pl.zst) DPAC_BWD2(DPAC_SCHEME_ADAPTIVE, true) else DPAC_BWD2(DPAC_SCHEME_ADAPTIVE, false)
+        } else {
+          if (pl.zst) DPAC_BWD2(DPAC_SCHEME_NAIVE, true) else DPAC_BWD2(DPAC_SCHEME_NAIVE, false)
+        }
+#undef DPAC_BWD2
+        break;
+      }
       if (adaptive) hipLaunchKernelGGL((k_rollout_nn_bwd<T, E, D, DPAC_SCHEME_ADAPTIVE>), ngrid, nblock, 0, s, eq, c, m, r);
       else hipLaunchKernelGGL((k_rollout_nn_bwd<T, E, D, DPAC_SCHEME_NAIVE>), ngrid, nblock, 0, s, eq, c, m, r);
       break;

@@ -13,18 +13,18 @@ struct Mfma;
 template <>
 struct Mfma<float> {
   using acc_t = __attribute__((ext_vector_type(4))) float;
-  __device__ static acc_t mma(float a, float b, acc_t c) {
+  __device__ __forceinline__ static acc_t mma(float a, float b, acc_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
   }
-  __device__ static int row(int lane, int i) { return (lane >> 4) * 4 + i; }
+  __device__ __forceinline__ static int row(int lane, int i) { return (lane >> 4) * 4 + i; }
 };
 template <>
 struct Mfma<double> {
   using acc_t = __attribute__((ext_vector_type(4))) double;
-  __device__ static acc_t mma(double a, double b, acc_t c) {
+  __device__ __forceinline__ static acc_t mma(double a, double b, acc_t c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
   }
-  __device__ static int row(int lane, int i) { return (lane >> 4) + 4 * i; }  // f64 C map
+  __device__ __forceinline__ static int row(int lane, int i) { return (lane >> 4) + 4 * i; }  // f64 C map
 };
 
 }  // namespace dpac

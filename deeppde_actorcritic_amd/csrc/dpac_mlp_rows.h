@@ -225,7 +225,7 @@ struct MrFwdEpi {
   T* out;           // output layer: out row 0 of the workgroup
   int64_t out_ld;
   template <int NT>
-  __device__ void finish(typename Mfma<T>::acc_t (&acc)[RT][NT], int wave, int lane) {
+  __device__ __forceinline__ void finish(typename Mfma<T>::acc_t (&acc)[RT][NT], int wave, int lane) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int col = (wave + kMrWaves * j) * 16 + (lane & 15);
@@ -267,7 +267,7 @@ struct MrBwdEpi {
   T* g;                    // G_l of row 0 of the workgroup
   int64_t g_ld;
   template <int NT>
-  __device__ void finish(typename Mfma<T>::acc_t (&acc)[RT][NT], int wave, int lane) {
+  __device__ __forceinline__ void finish(typename Mfma<T>::acc_t (&acc)[RT][NT], int wave, int lane) {
     T zz[NT][RT][4];
     if (scale) {  // all the z loads first, then the stores
 #pragma unroll

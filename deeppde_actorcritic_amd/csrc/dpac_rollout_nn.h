@@ -143,11 +143,84 @@ __device__ __forceinline__ void mfma_rows16_km(const float* in, int K, int Nout,
   }
 }
 
+#ifndef DPAC_NN_KMS
+#define DPAC_NN_KMS 1  // 1: static-K (fully unrolled) k-major layers for the specialised K16
+#endif
+#ifndef DPAC_NN_KMS_PG
+#define DPAC_NN_KMS_PG 2  // groups of B in flight per tile in the static-K layer (3, 4 measured slower)
+#endif
+
+// mfma_rows16_km with the group count NG = K16 / 16 a template constant: the K loop is
+// straight-line code, so the A operand of every group is read from LDS up front (NG
+// ds_read_b128, one wait), the B ring issues exactly the groups that exist (no
+// past-the-end loads) and every wait is a counted vmcnt.  Same products, same order.
+template <int NT, int NG, class EPI>
+__device__ __forceinline__ void mfma_rows16_kms(const float* in, int Nout, const float* Wkm, int wave,
+                                                int lane, EPI& epi) {
+  using MF = Mfma<float>;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  constexpr int K16 = 16 * NG;
+  constexpr int PG = DPAC_NN_KMS_PG < NG ? DPAC_NN_KMS_PG : NG;
+  const int col_l = lane & 15, kq = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wkm, (uint32_t)(Nout * K16 * 4));
+  uint32_t voff[NT];
+  MF::acc_t acc[NT];
+  typename EPI::Col cc[NT];
+  auto loadB = [&](int s, int j) {
+    uint32_t w[4];
+    buf_load_dwords<4>(rW, voff[j] + (uint32_t)(s * 64), w);
+    f4 v;
+    __builtin_memcpy(&v, &w[0], 16);
+    return v;
+  };
+  f4 b[PG][NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+    voff[j] = col < Nout ? (uint32_t)((col * K16 + 4 * kq) * 4) : kOOB;
+    acc[j] = MF::acc_t{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int q = 0; q < PG; ++q)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) b[q][j] = loadB(q, j);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+    cc[j] = epi.load(col, col < Nout);
+  }
+  const float* arow = in + col_l * kNnLd + 4 * kq;  // 16-byte aligned: kNnLd % 4 == 0
+  f4 a[NG];
+#pragma unroll
+  for (int s = 0; s < NG; ++s) a[s] = *reinterpret_cast<const f4*>(arow + 16 * s);
+#pragma unroll
+  for (int s = 0; s < NG; ++s) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[j] = MF::mma(a[s][e], b[s % PG][j][e], acc[j]);
+      if (s + PG < NG) b[s % PG][j] = loadB(s + PG, j);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) epi.store(i, MF::row(lane, i), col, col < Nout, acc[j][i], cc[j]);
+  }
+}
+
 template <typename T, int NT, class EPI>
 __device__ __forceinline__ void mfma_rows16(const T* in, int K, int Nout, const T* W, const T* Wkm,
                                             int wave, int lane, EPI& epi) {
   if constexpr (sizeof(T) == 4) {
     if (Wkm) {  // block-uniform
+#if DPAC_NN_KMS
+      // the actor shapes' K16 (d = 20 -> 32; hidden 200 -> 208) as straight-line layers
+      const int ng = (K + 15) / 16;
+      if (ng == 2) { mfma_rows16_kms<NT, 2>(in, Nout, Wkm, wave, lane, epi); return; }
+      if (ng == 13) { mfma_rows16_kms<NT, 13>(in, Nout, Wkm, wave, lane, epi); return; }
+#endif
       mfma_rows16_km<NT>(in, K, Nout, Wkm, wave, lane, epi);
       return;
     }
@@ -305,6 +378,11 @@ __device__ __forceinline__ void mfma_rows16_splitk(const T* in, int K, int Nout,
   if (ecol < NT * 16) epi.storeE(erow, ecol, evalid, v, ce);
 }
 
+// Whether mfma_layer runs the layer as the split-K product (two internal barriers).
+__device__ __forceinline__ bool nn_splitk_layer(int K, int Nout) {
+  return DPAC_NN_SPLITK && kNnWaves == 8 && Nout <= 32 && K > 32;
+}
+
 // Run mfma_rows16 with this wave's (wave-uniform) tile count.
 template <typename T, class EPI>
 __device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T* W, const T* Wkm,
@@ -344,17 +422,17 @@ struct FwdEpi {
   T* save;         // global row block of this layer's z, or null
   int64_t save_stride;
   int rows_live;
-  __device__ Col load(int col, bool valid) const {
+  __device__ __forceinline__ Col load(int col, bool valid) const {
     return Col{valid ? scale[col] : T(0), valid ? shift[col] : T(0),
                (valid && bias) ? bias[col] : T(0)};
   }
   // one element (split-K epilogue): the same constants and arithmetic
   using ColE = Col;
-  __device__ ColE loadE(int, int col, bool valid) const { return load(col, valid); }
-  __device__ void storeE(int row, int col, bool valid, T z, const ColE& k) const {
+  __device__ __forceinline__ ColE loadE(int, int col, bool valid) const { return load(col, valid); }
+  __device__ __forceinline__ void storeE(int row, int col, bool valid, T z, const ColE& k) const {
     store(0, row, col, valid, z, k);
   }
-  __device__ void store(int, int row, int col, bool valid, T z, const Col& k) const {
+  __device__ __forceinline__ void store(int, int row, int col, bool valid, T z, const Col& k) const {
     if (save && valid && row < rows_live) save[row * save_stride + col] = z;
     T yv = bias ? z + k.bb : z;          // addmm(b, y, W) (solver.py:270)
     yv = k.sh + yv * k.s;                // addcmul(beta, y, gamma/sqrt(1+eps))
@@ -380,7 +458,7 @@ struct BwdEpi {
   T* out;                  // LDS [16][kNnLd]
   T* g;                    // G_l of row 0 of the workgroup at this step
   int64_t g_stride;
-  __device__ Col load(int col, bool valid) const {
+  __device__ __forceinline__ Col load(int col, bool valid) const {
     Col k{};
     if (scale) {
       k.s = valid ? scale[col] : T(0);
@@ -400,7 +478,7 @@ struct BwdEpi {
   struct ColE {
     T s, sh, z;
   };
-  __device__ ColE loadE(int row, int col, bool valid) const {
+  __device__ __forceinline__ ColE loadE(int row, int col, bool valid) const {
     ColE k{};
     if (scale) {
       k.s = valid ? scale[col] : T(0);
@@ -409,7 +487,7 @@ struct BwdEpi {
     }
     return k;
   }
-  __device__ void storeE(int row, int col, bool valid, T acc, const ColE& k) const {
+  __device__ __forceinline__ void storeE(int row, int col, bool valid, T acc, const ColE& k) const {
     T v = acc;
     if (scale) {
       const T yv = k.sh + k.z * k.s;
@@ -420,7 +498,7 @@ struct BwdEpi {
 #endif
     out[row * kNnLd + col] = valid ? v : T(0);
   }
-  __device__ void store(int i, int row, int col, bool valid, T acc, const Col& k) const {
+  __device__ __forceinline__ void store(int i, int row, int col, bool valid, T acc, const Col& k) const {
     T v = acc;
     if (scale) {
       const T yv = k.sh + k.z[i] * k.s;  // the forward's BN_l output, same expression

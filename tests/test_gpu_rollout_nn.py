@@ -303,3 +303,50 @@ def test_fp32_kmajor_weights_match_row_major(name, d, hidden, B, monkeypatch):
         for a, b in zip(grads["on"], grads["off"]):
             scale = 1 + float(b.abs().max())
             assert float((a - b).abs().max()) <= 2e-3 * scale
+
+
+@pytest.mark.parametrize("name,d,hidden,B,dtype,scheme", [
+    ("LQR", 20, (200, 200, 200), 100, torch.float32, "adaptive"),
+    ("EKN", 20, (64, 64, 64), 37, torch.float32, "naive"),
+    ("VDP", 20, (48, 48), 37, torch.float64, "adaptive"),
+    ("LQR_var", 10, (32, 48, 24), 21, torch.float64, "naive"),
+    ("LQR", 20, (256, 256, 256, 256), 20, torch.float32, "adaptive"),
+    ("EKN", 5, (40, 40), 1, torch.float64, "adaptive")])
+def test_bptt_stager_writer_kernel_bitwise(name, d, hidden, B, dtype, scheme):
+    """k_rollout_nn_bwd2 (step inputs and z staged in LDS by a stager wavefront, G stored by
+    a writer wavefront) gives bitwise the G of k_rollout_nn_bwd (the same products in the
+    same order), partial tiles, the Eikonal head, both schemes, both dtypes."""
+    import os
+    N, T = 12, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme=scheme,
+                      dtype="float32" if dtype == torch.float32 else "float64")
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, _ = actor_pair(cfg, dtype)
+    eqp = ep.params()
+    sch = SCHEMES[scheme]
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=8, dtype=dtype, device=DEV)
+    y, disc, xN, saved = ops.actor_rollout_saves(eqp, sch, x0, dw, T, N, net)
+    x, u, dwc, z, flag, disc_t = saved
+    params = [p.detach() for p in net.trainable_variables()]
+    L = len(hidden)
+    gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
+    widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+    view, wt, wt_km = ops.mlp_prepare(gam, bet, Ws, b, net.ekn_head, True)
+    g_y = torch.full_like(y, 1.0 / B)
+    g_disc = torch.rand_like(y)
+    g_xN = torch.randn_like(xN)
+    out = {}
+    old = os.environ.get("DPAC_BPTT")
+    try:
+        for k in ("1", "2"):
+            os.environ["DPAC_BPTT"] = k
+            G = ops._bptt_fused(eqp, sch, T, N, L, x, u, dwc, z, flag, disc_t, view, wt, wt_km, widths,
+                                g_xN, g_disc, g_y)
+            out[k] = ops.G_all(G).clone()
+    finally:
+        if old is None:
+            os.environ.pop("DPAC_BPTT", None)
+        else:
+            os.environ["DPAC_BPTT"] = old
+    assert torch.isfinite(out["2"]).all()
+    assert torch.equal(out["1"], out["2"])
