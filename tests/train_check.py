@@ -66,12 +66,17 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "train_check.json"))
     ap.add_argument("--graphs", type=int, default=1,
                     help="1: the production path (HIP graphs, split critic/actor steps on side streams)")
+    ap.add_argument("--sampler", default="host", choices=["host", "device"],
+                    help="host: the reference's numpy stream (needed for the oracle); device: Philox "
+                         "drawn in float64 for every run and rounded to the run's dtype (long GPU runs)")
     ap.add_argument("--oracle-from", default=None,
                     help="reuse the oracle history of an earlier train_check JSON (same settings)")
     a = ap.parse_args()
     runs = a.runs.split(",")
+    if a.sampler == "device":
+        assert "oracle" not in runs and not a.oracle_from, "the oracle needs the host sampler's numpy stream"
     res = {"config": f"{a.config} (configs/{a.config}.json values)", "iters": a.iters, "log_freq": a.log_freq,
-           "batch": a.batch, "valid": a.valid, "graphs": bool(a.graphs), "runs": {}}
+           "batch": a.batch, "valid": a.valid, "graphs": bool(a.graphs), "sampler": a.sampler, "runs": {}}
     init = None
     for run in runs:
         if run == "oracle":
@@ -79,7 +84,14 @@ def main():
         dtype = "float32" if run == "gpu32" else "float64"
         cfg = lqr_d20(a.iters, a.log_freq, dtype, a.batch, a.valid, a.config)
         bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
-        sp = psol.ActorCriticSolver(cfg, bsde, seed=a.seed, sampler="host", graphs=bool(a.graphs))
+        sp = psol.ActorCriticSolver(cfg, bsde, seed=a.seed, sampler=a.sampler, graphs=bool(a.graphs))
+        if a.sampler == "device":  # same Philox keys in every run; increments drawn in float64
+            draw = bsde.sample_device
+
+            def sample64(kind, n, N, key, off=0, dtype=None, _draw=draw, _dt=sp.dtype):
+                b = _draw(kind, n, N, key, off, torch.float64)
+                return type(b)(*(t.to(_dt) for t in b))
+            bsde.sample_device = sample64
         if init is None:  # every run starts from the first run's weights, in float64
             init = {"critic": sp.model_critic.NN_value.export_params(),
                     "critic_grad": sp.model_critic.NN_value_grad.export_params(),
@@ -122,6 +134,13 @@ def main():
             r: float(np.max(np.abs(np.array(v["history"]["err_value"]) - ref)))
             for r, v in res["runs"].items() if r != "oracle"}
         print(json.dumps(res["max_abs_err_value_diff_vs_oracle"]), flush=True)
+    elif "gpu64" in res["runs"]:  # long runs: the fp64 product (5.6e-17 of the oracle) as the reference
+        ref = np.array(res["runs"]["gpu64"]["history"]["err_value"])
+        res["max_abs_err_value_diff_vs_gpu64"] = {
+            r: float(np.max(np.abs(np.array(v["history"]["err_value"]) - ref)))
+            for r, v in res["runs"].items() if r != "gpu64"}
+        res["final_err_value"] = {r: v["history"]["err_value"][-1] for r, v in res["runs"].items()}
+        print(json.dumps({k: res[k] for k in ("max_abs_err_value_diff_vs_gpu64", "final_err_value")}), flush=True)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
 

@@ -73,8 +73,9 @@ def main(tag):
         "correction": "FETCH_SIZE x2 (MI355X_MICROARCH.md §HBM), counters in KiB, separate --pmc passes",
     }
     json.dump(summary, open(os.path.join(PROF, f"{tag}_pmc_rollout.json"), "w"), indent=2)
-    json.dump({"rollout_adaptive_f32_B4096_N200_d20": {"hbm_bytes_per_launch": fetch_b + write_b,
-                                                        "source": f"profiles/{tag}_pmc_rollout.json"}},
+    # bench.py's PMC passes time the launches rotating over its 5 buffer sets (cold cache)
+    json.dump({"rollout_adaptive_f32_B4096_N200_d20_cold5": {"hbm_bytes_per_launch": fetch_b + write_b,
+                                                              "source": f"profiles/{tag}_pmc_rollout.json"}},
               open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=2)
     print(json.dumps(summary, indent=2))
 
