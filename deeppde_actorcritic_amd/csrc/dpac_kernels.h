@@ -93,12 +93,14 @@ struct DevConsts {
 #ifndef DPAC_ROLLOUT_KB_CAP
 #define DPAC_ROLLOUT_KB_CAP 8
 #endif
-// Cache-policy immediates of k_rollout's streamed dw loads and x stores (0 = default).
+// Cache-policy immediates of k_rollout's streamed dw loads and x stores (0 = default,
+// 2 = nt).  Measured with 5 rotating buffer sets (HBM, not Infinity-Cache resident):
+// nt x stores 39.8 -> 38.0 us at B = 4096, 146 -> 131 us at 16384; nt dw loads no gain.
 #ifndef DPAC_ROLLOUT_DW_AUX
 #define DPAC_ROLLOUT_DW_AUX 0
 #endif
 #ifndef DPAC_ROLLOUT_X_AUX
-#define DPAC_ROLLOUT_X_AUX 0
+#define DPAC_ROLLOUT_X_AUX 2
 #endif
 // KB = 0 (a frame larger than half the budget): no ring, each step loads its
 // own frame right before computing.
@@ -810,6 +812,15 @@ inline int bptt_kernel() {
   return (e && e[0] == '1') ? 1 : 2;
 }
 
+// Dynamic LDS of k_rollout_nn_bwd2: at least what it needs; DPAC_BPTT_LDS=max claims the
+// whole LDS so no other kernel's workgroup shares a BPTT CU (timing experiments).
+inline uint32_t bptt_lds(uint32_t need, uint32_t cap) {
+  const char* e = getenv("DPAC_BPTT_LDS");  // read per launch
+  if (!e) return need;
+  const uint32_t v = (e[0] == 'm') ? cap : (uint32_t)atoi(e);
+  return v > need ? (v < cap ? v : cap) : need;
+}
+
 inline int nn_tile_rows() {
   const char* e = getenv("DPAC_NN_TILE");  // read per launch: tests switch it in-process
   const int v = e ? atoi(e) : 0;
@@ -934,14 +945,15 @@ int run_op(const OpArgs& a) {
         int wsum = 0;
         for (int i = 0; i <= m.L + 1; ++i) wsum += m.width[i];
         const BwdPlan<T, D, E::CDIM> pl(wsum, m.ztot, true);
+        const uint32_t lds = bptt_lds(pl.total, BwdPlan<T, D, E::CDIM>::kMaxDyn);
         const dim3 nb2(kNnBwdThreads);
 #define DPAC_BWD2(SCH, ZS)                                                                          \
   {                                                                                                 \
     auto kfn = k_rollout_nn_bwd2<T, E, D, SCH, ZS>;                                                 \
     if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                      \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.total)) \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))     \
       return (int)e;                                                                                \
-    hipLaunchKernelGGL(kfn, ngrid, nb2, pl.total, s, eq, c, m, r);                                  \
+    hipLaunchKernelGGL(kfn, ngrid, nb2, lds, s, eq, c, m, r);                                       \
   }
         if (adaptive) {
           if (pl.zst) DPAC_BWD2(DPAC_SCHEME_ADAPTIVE, true) else DPAC_BWD2(DPAC_SCHEME_ADAPTIVE, false)

@@ -41,6 +41,24 @@ constexpr int kNnPrefetch = DPAC_NN_PREFETCH;
 #define DPAC_BWD_ABLATE 0  // timing-only BPTT builds (bits): 1 = no z loads, 2 = no G stores,
                            // 4 = no step-lane loads, 8 = skip the MLP chain
 #endif
+// Timing-only builds (-DDPAC_NN_TRACE=1): lane 0 of every wavefront of workgroup 0
+// records the shader clock at fixed points of the first 64 steps into a per-TU device
+// table, read back by dpac_debug_trace (tools/probe_trace.py).
+#ifndef DPAC_NN_TRACE
+#define DPAC_NN_TRACE 0
+#endif
+#if DPAC_NN_TRACE
+static __device__ uint32_t g_nn_trace[64 * 16 * 16];  // [step][wave][point]
+#define NN_MARK(t, pt)                                                                   \
+  do {                                                                                   \
+    if (blockIdx.x == 0 && lane == 0 && (t) < 64)                                        \
+      g_nn_trace[((t) * 16 + wave) * 16 + (pt)] = (uint32_t)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define NN_MARK(t, pt) \
+  do {               \
+  } while (0)
+#endif
 // The ring reads A up to k < 4 * roundup(ceil(K/4), kNnPrefetch) <= 256 for K <= 256.
 static_assert(DPAC_MLP_MAX_WIDTH <= 256 && kNnLd >= 256, "A reads stay inside an LDS row");
 
@@ -707,6 +725,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
   auto load = [&](int t, DwFrame<T, M>& fr) { sx.load(rs_dw, fr.dw, (uint32_t)t * slab); };
   auto body = [&](int t, DwFrame<T, M>& fr, auto) {
     __syncthreads();  // a0 of step t is in s_x0; the previous step's reads are done
+    NN_MARK(t, 0);
     // ---- actor MLP on MFMA (all four wavefronts) ----
     const T* in = s_x0;
     int pq = 0;
@@ -716,7 +735,9 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
                     a.save_z ? a.save_z + ((int64_t)t * a.B + row0) * mlp.ztot + mlp.zoff[l + 1] : nullptr,
                     mlp.ztot, rows_live};
       mfma_layer<T>(in, mlp.width[l], mlp.width[l + 1], mlp.weight[l], mlp.wkm[l], wave, lane, epi);
+      NN_MARK(t, 1 + 2 * l);
       __syncthreads();
+      NN_MARK(t, 2 + 2 * l);
       in = out;
       pq ^= 1;
     }
@@ -758,6 +779,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
       a.coef[lc.b * a.N + t] = cf;
     }
     write_a0(x);
+    NN_MARK(t, 15);
   };
   pipelined<KB, DwFrame<T, M>>(0, a.N, load, body);
   if constexpr (COST) {

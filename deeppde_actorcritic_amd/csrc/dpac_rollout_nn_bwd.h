@@ -263,6 +263,7 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
   for (int t = a.N - 1; t >= 0; --t) {
     const int64_t rowt = (int64_t)t * a.B;
     const int par = t & 1;
+    NN_MARK(t, 0);
     if (stager && t > 0) stage_in(t - 1, par ^ 1);  // lands while step t computes
     if (stepper) {
       const unsigned char* bi = s_in(par);
@@ -304,7 +305,9 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
       for (int m = 0; m < MC; ++m)
         if (ownu.valid(m)) lrow[ownu.j(m)] = gu[m];
     }
+    NN_MARK(t, 1);
     nn_bar();
+    NN_MARK(t, 2);
     if (stager && t > 0) stage_z(t - 1, par ^ 1, 0);
     if (writer)
       write_G_block(s_pq[0], mlp.width[L + 1], a.G + (rowt + row0) * a.gtot, a.gtot, a.goff[L + 1],
@@ -324,7 +327,9 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
         nn_bar();  // the split-K product's two internal barriers
         nn_bar();
       }
+      NN_MARK(t, 3 + 2 * (L - l));
       nn_bar();
+      NN_MARK(t, 4 + 2 * (L - l));
       if (stager && t > 0 && L - l + 1 < (int)kZParts) stage_z(t - 1, par ^ 1, (uint32_t)(L - l + 1));
       if (writer) write_G_block(out, Nout, a.G + (rowt + row0) * a.gtot, a.gtot, a.goff[l], rows_live, lane);
       in = out;
@@ -336,7 +341,9 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
         lam[m] = gxd[m] + (own.valid(m) ? in[g * kNnLd + own.j(m)] * s0[m] : T(0));
     }
     if (stager) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step t-1's inputs landed
+    NN_MARK(t, 13);
     nn_bar();
+    NN_MARK(t, 14);
   }
   if (a.g_x0 && live) own.store(a.g_x0 + lc.b * D, lam);
 }
