@@ -834,6 +834,7 @@ inline dim3 grid_for(int64_t B, int P) {
 
 template <typename T, class E, int D>
 int run_op(const OpArgs& a) {
+  constexpr bool kFastOk = std::is_same<T, float>::value;  // the NN fast path is float-only
   const E eq = E::make(a.eq);
   const DevConsts<T> c = DevConsts<T>::make(host_consts(a));
   constexpr int P = E::kP;
@@ -940,6 +941,8 @@ int run_op(const OpArgs& a) {
         r.wt[i] = (const T*)a.mlp_wt[i];
         r.wtkm[i] = (const T*)a.mlp.weight_km[i];  // k-major images of wt (dpac.h)
       }
+      // the fast path serves k_rollout_nn_bwd2 (the generic k_rollout_nn_bwd ignores it)
+      r.fast = nn_fast_host<T>(m.L, m.width, (const void* const*)r.wtkm, m.width[m.L + 1], m.width[0]);
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
       if (bptt_kernel() == 2) {
         int wsum = 0;
@@ -949,7 +952,7 @@ int run_op(const OpArgs& a) {
         const dim3 nb2(kNnBwdThreads);
 #define DPAC_BWD2(SCH, ZS)                                                                          \
   {                                                                                                 \
-    auto kfn = k_rollout_nn_bwd2<T, E, D, SCH, ZS>;                                                 \
+    auto kfn = r.fast ? k_rollout_nn_bwd2<T, E, D, SCH, ZS, kFastOk> : k_rollout_nn_bwd2<T, E, D, SCH, ZS, false>; \
     if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                      \
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))     \
       return (int)e;                                                                                \
@@ -985,6 +988,7 @@ int run_op(const OpArgs& a) {
         m.wkm[i] = (const T*)a.mlp.weight_km[i];
       }
       m.bias = (const T*)a.mlp.bias;
+      m.fast = nn_fast_host<T>(m.L, m.width, (const void* const*)m.wkm, m.width[0], m.width[m.L + 1]);
       NnRolloutArgs<T> r{};
       r.B = a.B; r.N = a.N; r.cost_order = a.cost_order;
       r.x0 = (const T*)a.x0; r.dw = (const T*)a.dw;
@@ -1015,8 +1019,11 @@ int run_op(const OpArgs& a) {
         }
       }
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
-#define DPAC_ROLL_NN(SCH, CO) \
-  hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1>), ngrid, nblock, 0, s, eq, c, m, r)
+#define DPAC_ROLL_NN(SCH, CO)                                                                                   \
+  do {                                                                                                          \
+    if (m.fast) hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1, kFastOk>), ngrid, nblock, 0, s, eq, c, m, r); \
+    else hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1, false>), ngrid, nblock, 0, s, eq, c, m, r);      \
+  } while (0)
       if (adaptive) {
         if (cost) DPAC_ROLL_NN(DPAC_SCHEME_ADAPTIVE, true); else DPAC_ROLL_NN(DPAC_SCHEME_ADAPTIVE, false);
       } else {

@@ -21,6 +21,9 @@ constexpr int kMrThreads = 256;
 constexpr int kMrWaves = 4;
 constexpr int kMrLd = DPAC_MLP_MAX_WIDTH + 4;  // LDS row stride: 16 rows x 4 k hit 64 banks
 constexpr int kMrPrefetch = 8;
+#ifndef DPAC_MR_PIN
+#define DPAC_MR_PIN 0  // sched_barrier after each k group of the k-major layers (timing knob)
+#endif
 
 template <typename T>
 struct MrCfg;
@@ -176,6 +179,9 @@ __device__ __forceinline__ void mr_layer_nt_km(const float* in, int K, int Nout,
           for (int rt = 0; rt < RT; ++rt) acc[rt][j] = MF::mma(av[q][rt][e], bq[q][j][e], acc[rt][j]);
         bq[q][j] = loadB(s0 + q + PG, j);
       }
+#if DPAC_MR_PIN
+      __builtin_amdgcn_sched_barrier(0);  // keep the B ring PG groups ahead (dpac_rollout_nn.h)
+#endif
     }
 #pragma unroll
     for (int q = 0; q < PG; ++q)

@@ -74,6 +74,7 @@ struct NnMlp {
   const T* weight[DPAC_MLP_MAX_HIDDEN + 1];
   const T* wkm[DPAC_MLP_MAX_HIDDEN + 1];  // k-major images of weight (optional, float)
   const T* bias;
+  int fast;  // the actor-shape fast path applies (nn_fast_host)
 };
 
 template <typename T>
@@ -164,6 +165,9 @@ __device__ __forceinline__ void mfma_rows16_km(const float* in, int K, int Nout,
 #ifndef DPAC_NN_KMS
 #define DPAC_NN_KMS 1  // 1: static-K (fully unrolled) k-major layers for the specialised K16
 #endif
+#ifndef DPAC_NN_PIN
+#define DPAC_NN_PIN 1  // sched_barrier after each k group of the static-K layers
+#endif
 #ifndef DPAC_NN_KMS_PG
 #define DPAC_NN_KMS_PG 2  // groups of B in flight per tile in the static-K layer (3, 4 measured slower)
 #endif
@@ -211,17 +215,23 @@ __device__ __forceinline__ void mfma_rows16_kms(const float* in, int Nout, const
     cc[j] = epi.load(col, col < Nout);
   }
   const float* arow = in + col_l * kNnLd + 4 * kq;  // 16-byte aligned: kNnLd % 4 == 0
-  f4 a[NG];
+  constexpr int AG = 4;  // A groups read ahead from LDS
+  f4 a[AG];
 #pragma unroll
-  for (int s = 0; s < NG; ++s) a[s] = *reinterpret_cast<const f4*>(arow + 16 * s);
+  for (int s = 0; s < AG && s < NG; ++s) a[s] = *reinterpret_cast<const f4*>(arow + 16 * s);
 #pragma unroll
   for (int s = 0; s < NG; ++s) {
+    const f4 as = a[s % AG];
+    if (s + AG < NG) a[s % AG] = *reinterpret_cast<const f4*>(arow + 16 * (s + AG));
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[j] = MF::mma(a[s][e], b[s % PG][j][e], acc[j]);
+      for (int e = 0; e < 4; ++e) acc[j] = MF::mma(as[e], b[s % PG][j][e], acc[j]);
       if (s + PG < NG) b[s % PG][j] = loadB(s + PG, j);
     }
+#if DPAC_NN_PIN
+    __builtin_amdgcn_sched_barrier(0);  // keep the B ring's loads PG groups ahead (see kms_pre)
+#endif
   }
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
@@ -430,6 +440,258 @@ __device__ __forceinline__ void mfma_layer(const T* in, int K, int Nout, const T
   }
 }
 
+// ---------------------------------------------------------------------------
+// Actor-shape fast path (float, k-major weight images): the BASELINE actors are
+// d -> 200 -> 200 -> 200 -> c with d, c <= 32.  The clock trace of one step
+// (profiles/r02_nn_phase_trace_base.json, B = 2048) shows the two narrow layers —
+// 0.4 us of MFMA work each — taking 1.5-1.8 us of wall time, and every layer
+// starting with an L2 round trip for its first weights.  So:
+//  * the narrow layers' B fragments stay in VGPRs for the whole launch: the
+//    narrow-K layer (K16 <= 32, e.g. 20 -> 200) as NG groups of this wave's NT <= 2
+//    tiles, the narrow-output split-K layer (e.g. 200 -> 20) as this wave's two
+//    16-k groups of its K slice — 16 VGPRs each;
+//  * a wide layer's first PG groups of weights are loaded before the barrier that
+//    precedes it (weights do not depend on the activations), into 16 VGPRs.
+// The products are the same, in the same order, as mfma_layer's: bitwise equal.
+// ---------------------------------------------------------------------------
+typedef float nnf4 __attribute__((ext_vector_type(4)));
+
+struct NarrowIn {   // B of a K16 <= 32 layer: [group s][tile j], tiles j >= mine read 0
+  nnf4 b[2][2];
+};
+struct NarrowOut {  // B of the split-K layer: [group g of the wave's K slice][tile j]
+  nnf4 b[2][2];
+};
+struct WidePre {    // the first DPAC_NN_KMS_PG groups of a wide layer's B
+  nnf4 b[DPAC_NN_KMS_PG][2];
+};
+
+__device__ __forceinline__ nnf4 nn_load_f4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  uint32_t w[4];
+  buf_load_dwords<4>(r, off, w);
+  nnf4 v;
+  __builtin_memcpy(&v, &w[0], 16);
+  return v;
+}
+
+// this wave's tile count of an Nout-wide column split
+__device__ __forceinline__ int nn_mine(int Nout, int wave) {
+  const int ntiles = (Nout + 15) / 16;
+  return ntiles > wave ? (ntiles - wave + kNnWaves - 1) / kNnWaves : 0;
+}
+
+__device__ __forceinline__ void load_narrow_in(NarrowIn& r, const float* Wkm, int K, int Nout, int wave,
+                                               int lane) {
+  const int col_l = lane & 15, kq = lane >> 4;
+  const int K16 = (K + 15) / 16 * 16;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wkm, (uint32_t)(Nout * K16 * 4));
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      r.b[s][j] = nn_load_f4(rW, (col < Nout && 16 * s < K16) ? (uint32_t)((col * K16 + 4 * kq + 16 * s) * 4) : kOOB);
+  }
+}
+
+__device__ __forceinline__ void load_narrow_out(NarrowOut& r, const float* Wkm, int K, int Nout, int wave,
+                                                int lane) {
+  const int col_l = lane & 15, kq = lane >> 4;
+  const int K16 = (K + 15) / 16 * 16;
+  const __amdgpu_buffer_rsrc_t rK = make_rsrc(Wkm, (uint32_t)(Nout * K16 * 4));
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int kb = wave * 32 + 16 * g;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = j * 16 + col_l;
+      r.b[g][j] = nn_load_f4(rK, (col < Nout && kb < K16) ? (uint32_t)((col * K16 + kb + 4 * kq) * 4) : kOOB);
+    }
+  }
+}
+
+// the first PG groups of the wide layer (K, Nout) this wave will multiply
+__device__ __forceinline__ void load_wide_pre(WidePre& r, const float* Wkm, int K, int Nout, int wave, int lane) {
+  const int col_l = lane & 15, kq = lane >> 4;
+  const int K16 = (K + 15) / 16 * 16;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wkm, (uint32_t)(Nout * K16 * 4));
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+#pragma unroll
+    for (int q = 0; q < DPAC_NN_KMS_PG; ++q)
+      r.b[q][j] = nn_load_f4(rW, col < Nout ? (uint32_t)((col * K16 + 4 * kq + 16 * q) * 4) : kOOB);
+  }
+}
+
+// mfma_rows16_kms<NT, NG> for NG <= 2 with B from registers (no weight loads)
+template <int NT, int NG, class EPI>
+__device__ __forceinline__ void mfma_rows16_res(const float* in, int Nout, const NarrowIn& r, int wave, int lane,
+                                                EPI& epi) {
+  using MF = Mfma<float>;
+  const int col_l = lane & 15, kq = lane >> 4;
+  MF::acc_t acc[NT];
+  typename EPI::Col cc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+    acc[j] = MF::acc_t{0, 0, 0, 0};
+    cc[j] = epi.load(col, col < Nout);
+  }
+  const float* arow = in + col_l * kNnLd + 4 * kq;
+  nnf4 a[NG];
+#pragma unroll
+  for (int s = 0; s < NG; ++s) a[s] = *reinterpret_cast<const nnf4*>(arow + 16 * s);
+#pragma unroll
+  for (int s = 0; s < NG; ++s)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[j] = MF::mma(a[s][e], r.b[s][j][e], acc[j]);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) epi.store(i, MF::row(lane, i), col, col < Nout, acc[j][i], cc[j]);
+  }
+}
+
+// mfma_rows16_kms<NT, NG> with its first PG groups of B already in registers
+template <int NT, int NG, class EPI>
+__device__ __forceinline__ void mfma_rows16_kms_pre(const float* in, int Nout, const float* Wkm, const WidePre& pre,
+                                                    int wave, int lane, EPI& epi) {
+  using MF = Mfma<float>;
+  constexpr int K16 = 16 * NG;
+  constexpr int PG = DPAC_NN_KMS_PG < NG ? DPAC_NN_KMS_PG : NG;
+  static_assert(PG == DPAC_NN_KMS_PG, "the prefetch holds PG groups");
+  const int col_l = lane & 15, kq = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wkm, (uint32_t)(Nout * K16 * 4));
+  uint32_t voff[NT];
+  MF::acc_t acc[NT];
+  typename EPI::Col cc[NT];
+  nnf4 b[PG][NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+    voff[j] = col < Nout ? (uint32_t)((col * K16 + 4 * kq) * 4) : kOOB;
+    acc[j] = MF::acc_t{0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < PG; ++q) b[q][j] = pre.b[q][j];
+    cc[j] = epi.load(col, col < Nout);
+  }
+  // A from LDS through a ring of AG groups (not all NG up front: 36 fewer VGPRs, which
+  // the 10-wavefront BPTT workgroup, capped at 168, needs for the resident narrow layers)
+  constexpr int AG = 4;
+  const float* arow = in + col_l * kNnLd + 4 * kq;
+  nnf4 a[AG];
+#pragma unroll
+  for (int s = 0; s < AG && s < NG; ++s) a[s] = *reinterpret_cast<const nnf4*>(arow + 16 * s);
+#pragma unroll
+  for (int s = 0; s < NG; ++s) {
+    const nnf4 as = a[s % AG];
+    if (s + AG < NG) a[s % AG] = *reinterpret_cast<const nnf4*>(arow + 16 * (s + AG));
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[j] = MF::mma(as[e], b[s % PG][j][e], acc[j]);
+      if (s + PG < NG) b[s % PG][j] = nn_load_f4(rW, voff[j] + (uint32_t)((s + PG) * 64));
+    }
+    // pin the ring: without this the scheduler sinks each load next to its first use
+    // (one load in flight, the L2 latency exposed every 4 MFMAs)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = (wave + kNnWaves * j) * 16 + col_l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) epi.store(i, MF::row(lane, i), col, col < Nout, acc[j][i], cc[j]);
+  }
+}
+
+// mfma_rows16_splitk's k-major branch with the wave's slice of B in registers
+template <int NT, class EPI>
+__device__ __forceinline__ void mfma_rows16_splitk_res(const float* in, int K, int Nout, const NarrowOut& r,
+                                                       int wave, int lane, EPI& epi, float* part) {
+  using MF = Mfma<float>;
+  const int col_l = lane & 15, kq = lane >> 4;
+  const int tid = wave * 64 + lane, erow = tid >> 5, ecol = tid & 31;
+  const bool evalid = ecol < Nout;
+  const typename EPI::ColE ce = epi.loadE(erow, ecol, evalid);
+  const int K16 = (K + 15) / 16 * 16;
+  MF::acc_t acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = MF::acc_t{0, 0, 0, 0};
+  nnf4 ak[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int kb = wave * 32 + 16 * g;
+    ak[g] = kb < K16 ? *reinterpret_cast<const nnf4*>(in + col_l * kNnLd + kb + 4 * kq) : nnf4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[j] = MF::mma(ak[g][e], r.b[g][j][e], acc[j]);
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[(wave * 16 + MF::row(lane, i)) * 32 + j * 16 + col_l] = acc[j][i];
+  __syncthreads();
+  float v = part[erow * 32 + ecol];
+#pragma unroll
+  for (int w = 1; w < kNnWaves; ++w) v += part[(w * 16 + erow) * 32 + ecol];
+  __syncthreads();
+  if (ecol < NT * 16) epi.storeE(erow, ecol, evalid, v, ce);
+}
+
+// Whether a network takes the fast path (host side, per launch): float k-major images, a
+// narrow first product (K16 <= 32), hidden layers of 13 column tiles (193..208 wide), a
+// split-K last product.  `kin` / `kout`: the widths entering the first / leaving the last
+// product in the kernel's layer order (forward: width[0] / width[L+1]; BPTT: reversed).
+// DPAC_NN_FAST=0 forces the generic path (tests compare the two bit for bit).
+template <typename T>
+inline bool nn_fast_host(int L, const int* width, const void* const* km, int kin, int kout) {
+  if (!std::is_same<T, float>::value || L < 1 || kin > 32 || kout > 32 || kNnWaves != 8 || !DPAC_NN_SPLITK)
+    return false;
+  const char* e = getenv("DPAC_NN_FAST");  // read per launch
+  if (e && e[0] == '0') return false;
+  for (int i = 1; i <= L; ++i)
+    if ((width[i] + 15) / 16 != 13) return false;
+  for (int i = 0; i <= L; ++i)
+    if (!km[i]) return false;
+  return true;
+}
+
+// the narrow-K product with resident B: this wave's tile count, NG in {1, 2}
+template <class EPI>
+__device__ __forceinline__ void nn_layer_narrow_in(const float* in, int K, int Nout, const NarrowIn& r, int wave,
+                                                   int lane, EPI& epi) {
+  const int mine = nn_mine(Nout, wave);
+  if (K <= 16) {
+    if (mine == 1) mfma_rows16_res<1, 1>(in, Nout, r, wave, lane, epi);
+    else if (mine == 2) mfma_rows16_res<2, 1>(in, Nout, r, wave, lane, epi);
+  } else {
+    if (mine == 1) mfma_rows16_res<1, 2>(in, Nout, r, wave, lane, epi);
+    else if (mine == 2) mfma_rows16_res<2, 2>(in, Nout, r, wave, lane, epi);
+  }
+}
+
+template <class EPI>
+__device__ __forceinline__ void nn_layer_wide(const float* in, int Nout, const float* Wkm, const WidePre& pre,
+                                              int wave, int lane, EPI& epi) {
+  const int mine = nn_mine(Nout, wave);
+  if (mine == 1) mfma_rows16_kms_pre<1, 13>(in, Nout, Wkm, pre, wave, lane, epi);
+  else if (mine == 2) mfma_rows16_kms_pre<2, 13>(in, Nout, Wkm, pre, wave, lane, epi);
+}
+
+template <class EPI>
+__device__ __forceinline__ void nn_layer_narrow_out(const float* in, int K, int Nout, const NarrowOut& r, int wave,
+                                                    int lane, EPI& epi) {
+  if (Nout <= 16) mfma_rows16_splitk_res<1>(in, K, Nout, r, wave, lane, epi, epi.out);
+  else mfma_rows16_splitk_res<2>(in, K, Nout, r, wave, lane, epi, epi.out);
+}
+
 // Forward epilogue of a dense layer: z -> (save z) -> BN(z (+ b)) -> [y + relu(y)]
 // into the next layer's LDS input.  Padding columns are written as 0.
 template <typename T>
@@ -544,6 +806,7 @@ struct NnBackArgs {
   const T* wtkm[DPAC_MLP_MAX_HIDDEN + 1];  // their k-major images (optional, float)
   int goff[DPAC_MLP_MAX_HIDDEN + 2];     // column offset of G_i in a G row
   int gtot;
+  int fast;  // the actor-shape fast path applies to the transposed chain (nn_fast_host)
 };
 
 // The actor's BPTT through a fused NN rollout, as one launch: the reverse time
@@ -663,7 +926,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd(const E eq, const
   if (a.g_x0 && live) own.store(a.g_x0 + lc.b * D, lam);
 }
 
-template <typename T, class E, int D, int SCHEME, bool COST, int KB>
+template <typename T, class E, int D, int SCHEME, bool COST, int KB, bool FAST>
 __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const DevConsts<T> c,
                                                           const NnMlp<T> mlp,
                                                           const NnRolloutArgs<T> a) {
@@ -719,6 +982,15 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
   T r = TR::kRadius ? dsqrt(Lanes<P>::sum(sumsq(x))) : T(0);
   Flags fl = SCHEME == DPAC_SCHEME_ADAPTIVE ? region(r, c) : Flags{true, false};
   T disc = 1, y = 0;
+  // fast path: the narrow layers' weights in registers for the whole launch
+  NarrowIn res_in;
+  NarrowOut res_out;
+  WidePre pre;
+  static_assert(!FAST || std::is_same<T, float>::value, "the fast path is float-only");
+  if constexpr (FAST) {  // launched only when mlp.fast (nn_fast_host)
+    load_narrow_in(res_in, mlp.wkm[0], mlp.width[0], mlp.width[1], wave, lane);
+    load_narrow_out(res_out, mlp.wkm[L], mlp.width[L], mlp.width[L + 1], wave, lane);
+  }
   __syncthreads();  // padding zeroed before the first a0 write
   write_a0(x);
 
@@ -734,7 +1006,19 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
       FwdEpi<T> epi{mlp.scale[l + 1], mlp.shift[l + 1], l == L ? mlp.bias : nullptr, l < L, out,
                     a.save_z ? a.save_z + ((int64_t)t * a.B + row0) * mlp.ztot + mlp.zoff[l + 1] : nullptr,
                     mlp.ztot, rows_live};
-      mfma_layer<T>(in, mlp.width[l], mlp.width[l + 1], mlp.weight[l], mlp.wkm[l], wave, lane, epi);
+      if constexpr (FAST) {
+        if (l == 0) {
+          if (L >= 2) load_wide_pre(pre, mlp.wkm[1], mlp.width[1], mlp.width[2], wave, lane);
+          nn_layer_narrow_in(in, mlp.width[0], mlp.width[1], res_in, wave, lane, epi);
+        } else if (l == L) {
+          nn_layer_narrow_out(in, mlp.width[L], mlp.width[L + 1], res_out, wave, lane, epi);
+        } else {
+          nn_layer_wide(in, mlp.width[l + 1], mlp.wkm[l], pre, wave, lane, epi);
+          if (l + 1 < L) load_wide_pre(pre, mlp.wkm[l + 1], mlp.width[l + 1], mlp.width[l + 2], wave, lane);
+        }
+      } else {
+        mfma_layer<T>(in, mlp.width[l], mlp.width[l + 1], mlp.weight[l], mlp.wkm[l], wave, lane, epi);
+      }
       NN_MARK(t, 1 + 2 * l);
       __syncthreads();
       NN_MARK(t, 2 + 2 * l);

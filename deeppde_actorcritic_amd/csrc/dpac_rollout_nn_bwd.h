@@ -21,6 +21,9 @@
 // Included by dpac_kernels.h inside namespace dpac, after dpac_rollout_nn.h.
 
 constexpr int kNnBwdThreads = kNnThreads + 128;  // + stager + writer
+#ifndef DPAC_BWD2_ZREG
+#define DPAC_BWD2_ZREG 0  // timing knob: stage z through the stager's VGPRs instead of LDS-DMA
+#endif
 #ifndef DPAC_BWD2_ABLATE
 #define DPAC_BWD2_ABLATE 0  // timing-only builds (bits): 1 = the stager copies nothing, 2 = the writer
                            // does nothing, 4 = the writer reads LDS but stores nothing
@@ -187,7 +190,7 @@ __device__ __forceinline__ void write_G_block(const T* img, int width, T* G, int
       write_G_rows<T, 1>(img + c0, width - c0 < 64 ? width - c0 : 64, G, gtot, goff + c0, rows_live, lane);
 }
 
-template <typename T, class E, int D, int SCHEME, bool ZST>
+template <typename T, class E, int D, int SCHEME, bool ZST, bool FAST>
 __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, const DevConsts<T> c,
                                                                   const NnMlp<T> mlp,
                                                                   const NnBackArgs<T> a) {
@@ -230,8 +233,30 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
   auto stage_z = [&](int ts, int par, uint32_t part) {
     if constexpr (ZST) {
       const int64_t rt = (int64_t)ts * a.B + row0;
+#if DPAC_BWD2_ZREG
+      // timing knob: the z share through the stager's VGPRs (dwordx4 loads, ds_write_b128)
+      // instead of LDS-DMA
+      const uint32_t bytes = (uint32_t)(rows_live * mlp.ztot * sizeof(T));
+      const uint32_t pieces = (bytes + 1023) / 1024;
+      const uint32_t k0 = pieces * part / kZParts, k1 = pieces * (part + 1) / kZParts;
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z + rt * mlp.ztot, bytes);
+      unsigned char* dst = s_dyn + pl.z + (uint32_t)par * pl.zpar;
+      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+      u4 v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t off = ((k0 + q) * 64 + (uint32_t)lane) * 16;
+        uint32_t w[4];
+        buf_load_dwords<4>(rz, (k0 + q < k1) ? off : kOOB, w);
+        v[q] = u4{w[0], w[1], w[2], w[3]};
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (k0 + q < k1) *reinterpret_cast<u4*>(dst + ((k0 + q) * 64 + (uint32_t)lane) * 16) = v[q];
+#else
       wave_copy_lds<16>(a.z + rt * mlp.ztot, (uint32_t)(rows_live * mlp.ztot * sizeof(T)),
                         s_dyn + pl.z + (uint32_t)par * pl.zpar, lane, part, kZParts);
+#endif
     }
   };
 
@@ -250,6 +275,17 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
     s0[m] = own.valid(m) ? mlp.scale[0][own.j(m)] : T(0);
     lam[m] = T(0);
     gxd[m] = T(0);
+  }
+  // fast path: the narrow products' weights in registers for the whole launch
+  NarrowIn res_in;
+  NarrowOut res_out;
+  WidePre pre;
+  static_assert(!FAST || std::is_same<T, float>::value, "the fast path is float-only");
+  if constexpr (FAST) {  // launched only when a.fast (nn_fast_host)
+    if (wave < kNnWaves) {
+      load_narrow_in(res_in, a.wtkm[L], mlp.width[L + 1], mlp.width[L], wave, lane);
+      load_narrow_out(res_out, a.wtkm[0], mlp.width[1], mlp.width[0], wave, lane);
+    }
   }
   if (a.g_xN && stepper) own.load_masked(a.g_xN + lc.b * D, lam);
   T gD = (a.g_disc && stepper) ? a.g_disc[lc.b] : T(0);
@@ -322,7 +358,19 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
         BwdEpiL<T> epi{l >= 1 ? s_bn + a.goff[l] : nullptr, l >= 1 ? s_bn + wsum + a.goff[l] : nullptr,
                        ZST ? s_z(par) + mlp.zoff[l] : a.z + (rowt + row0) * mlp.ztot + mlp.zoff[l],
                        mlp.ztot, rows_live, lane, out};
-        mfma_layer<T>(in, K, Nout, a.wt[l], a.wtkm[l], wave, lane, epi);
+        if constexpr (FAST) {
+          if (l == L) {
+            if (L >= 2) load_wide_pre(pre, a.wtkm[L - 1], mlp.width[L], mlp.width[L - 1], wave, lane);
+            nn_layer_narrow_in(in, K, Nout, res_in, wave, lane, epi);
+          } else if (l == 0) {
+            nn_layer_narrow_out(in, K, Nout, res_out, wave, lane, epi);
+          } else {
+            nn_layer_wide(in, Nout, a.wtkm[l], pre, wave, lane, epi);
+            if (l >= 2) load_wide_pre(pre, a.wtkm[l - 1], mlp.width[l], mlp.width[l - 1], wave, lane);
+          }
+        } else {
+          mfma_layer<T>(in, K, Nout, a.wt[l], a.wtkm[l], wave, lane, epi);
+        }
       } else if (nn_splitk_layer(K, Nout)) {
         nn_bar();  // the split-K product's two internal barriers
         nn_bar();

@@ -350,3 +350,55 @@ def test_bptt_stager_writer_kernel_bitwise(name, d, hidden, B, dtype, scheme):
             os.environ["DPAC_BPTT"] = old
     assert torch.isfinite(out["2"]).all()
     assert torch.equal(out["1"], out["2"])
+
+
+@pytest.mark.parametrize("name,d,hidden,B,scheme", [
+    ("LQR", 20, (200, 200, 200), 100, "adaptive"),
+    ("EKN", 20, (200, 200, 200), 37, "naive"),
+    ("VDP", 20, (200, 200), 50, "adaptive"),
+    ("LQR", 4, (208, 200, 193), 20, "adaptive"),
+    ("LQR_var", 20, (200,), 17, "naive")])
+def test_actor_fast_path_bitwise(name, d, hidden, B, scheme):
+    """The actor-shape fast path (narrow layers' weights resident in VGPRs, wide layers'
+    first weight groups loaded before the preceding barrier) gives bitwise the outputs of
+    the generic layer code, in the fused forward (16-row tiles) and in the BPTT kernel:
+    K16 = 16 and 32 first products, 193..208-wide hidden layers, 1-3 hidden layers, the
+    Eikonal head (21 outputs), VDP's 10 controls."""
+    import os
+    N, T = 12, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme=scheme, dtype="float32")
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, _ = actor_pair(cfg, torch.float32)
+    eqp = ep.params()
+    sch = SCHEMES[scheme]
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=9, dtype=torch.float32, device=DEV)
+    params = [p.detach() for p in net.trainable_variables()]
+    L = len(hidden)
+    gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
+    widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+    view, wt, wt_km = ops.mlp_prepare(gam, bet, Ws, b, net.ekn_head, True)
+    g_y = torch.full((B,), 1.0 / B, device=DEV)
+    keys = ("DPAC_NN_FAST", "DPAC_NN_TILE")
+    old = {k: os.environ.get(k) for k in keys}
+    fwd, bwd = {}, {}
+    try:
+        os.environ["DPAC_NN_TILE"] = "16"
+        for f in ("0", "1"):
+            os.environ["DPAC_NN_FAST"] = f
+            fwd[f] = [t.clone() if torch.is_tensor(t) else [s.clone() for s in t]
+                      for t in ops.rollout_nn(eqp, sch, x0, dw, T, N, view, cost_order=_lib.COST_ACTOR, save=True)]
+            x, _, _, u, _, _, (z, flag, disc_t) = fwd[f]
+            G = ops._bptt_fused(eqp, sch, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km, widths,
+                                torch.ones_like(x[-1]) * 0.01, torch.full_like(g_y, 0.5), g_y)
+            bwd[f] = ops.G_all(G).clone()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for a, b in zip(fwd["0"], fwd["1"]):
+        for s, t in (zip(a, b) if isinstance(a, list) else [(a, b)]):
+            assert torch.equal(s, t)
+    assert torch.isfinite(bwd["1"]).all()
+    assert torch.equal(bwd["0"], bwd["1"])
