@@ -525,9 +525,13 @@ __device__ __forceinline__ void load_wide_pre(WidePre& r, const float* Wkm, int 
 }
 
 // mfma_rows16_kms<NT, NG> for NG <= 2 with B from registers (no weight loads)
-template <int NT, int NG, class EPI>
+struct NoMark {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <int NT, int NG, class EPI, class MK = NoMark>
 __device__ __forceinline__ void mfma_rows16_res(const float* in, int Nout, const NarrowIn& r, int wave, int lane,
-                                                EPI& epi) {
+                                                EPI& epi, MK mk = MK{}) {
   using MF = Mfma<float>;
   const int col_l = lane & 15, kq = lane >> 4;
   MF::acc_t acc[NT];
@@ -542,12 +546,20 @@ __device__ __forceinline__ void mfma_rows16_res(const float* in, int Nout, const
   nnf4 a[NG];
 #pragma unroll
   for (int s = 0; s < NG; ++s) a[s] = *reinterpret_cast<const nnf4*>(arow + 16 * s);
+#if DPAC_NN_TRACE
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  mk(10);  // A in registers
+#endif
 #pragma unroll
   for (int s = 0; s < NG; ++s)
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[j] = MF::mma(a[s][e], r.b[s][j][e], acc[j]);
+#if DPAC_NN_TRACE
+  asm volatile("" ::"v"(acc[NT - 1][3]));
+  mk(11);  // products done
+#endif
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = (wave + kNnWaves * j) * 16 + col_l;
@@ -664,16 +676,16 @@ inline bool nn_fast_host(int L, const int* width, const void* const* km, int kin
 }
 
 // the narrow-K product with resident B: this wave's tile count, NG in {1, 2}
-template <class EPI>
+template <class EPI, class MK = NoMark>
 __device__ __forceinline__ void nn_layer_narrow_in(const float* in, int K, int Nout, const NarrowIn& r, int wave,
-                                                   int lane, EPI& epi) {
+                                                   int lane, EPI& epi, MK mk = MK{}) {
   const int mine = nn_mine(Nout, wave);
   if (K <= 16) {
-    if (mine == 1) mfma_rows16_res<1, 1>(in, Nout, r, wave, lane, epi);
-    else if (mine == 2) mfma_rows16_res<2, 1>(in, Nout, r, wave, lane, epi);
+    if (mine == 1) mfma_rows16_res<1, 1>(in, Nout, r, wave, lane, epi, mk);
+    else if (mine == 2) mfma_rows16_res<2, 1>(in, Nout, r, wave, lane, epi, mk);
   } else {
-    if (mine == 1) mfma_rows16_res<1, 2>(in, Nout, r, wave, lane, epi);
-    else if (mine == 2) mfma_rows16_res<2, 2>(in, Nout, r, wave, lane, epi);
+    if (mine == 1) mfma_rows16_res<1, 2>(in, Nout, r, wave, lane, epi, mk);
+    else if (mine == 2) mfma_rows16_res<2, 2>(in, Nout, r, wave, lane, epi, mk);
   }
 }
 
@@ -1009,7 +1021,8 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
       if constexpr (FAST) {
         if (l == 0) {
           if (L >= 2) load_wide_pre(pre, mlp.wkm[1], mlp.width[1], mlp.width[2], wave, lane);
-          nn_layer_narrow_in(in, mlp.width[0], mlp.width[1], res_in, wave, lane, epi);
+          nn_layer_narrow_in(in, mlp.width[0], mlp.width[1], res_in, wave, lane, epi,
+                             [&](int pt) { NN_MARK(t, pt); });
         } else if (l == L) {
           nn_layer_narrow_out(in, mlp.width[L], mlp.width[L + 1], res_out, wave, lane, epi);
         } else {
