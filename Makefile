@@ -47,3 +47,35 @@ $(LIB): $(OBJS)
 
 clean:
 	rm -rf build $(LIB)
+
+# Host-side sanitizer run of the C-ABI validation layer (no GPU needed): every TU with
+# AddressSanitizer + UndefinedBehaviorSanitizer on the host side only (device code is
+# unchanged), d = 20 kernels, linked into build/asan/libdpac_asan.so, driven by
+# tests/abi_sanitize.c.   make sanitize   (log: build/asan/abi_sanitize.log)
+ASAN_DIR  := build/asan
+ASAN_HOST := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+             -Xarch_host -fno-omit-frame-pointer -Xarch_host -fno-sanitize-recover=undefined
+ASAN_FLAGS := $(filter-out -DDPAC_DIMS=% -DDPAC_DIMS_EVEN=%,$(HIPFLAGS)) -DDPAC_DIMS=20 -DDPAC_DIMS_EVEN=20 -O1 $(ASAN_HOST)
+ASAN_OBJS := $(ASAN_DIR)/dpac_abi.o $(ASAN_DIR)/dpac_mlp.o $(ASAN_DIR)/dpac_params.o \
+             $(foreach e,$(EQNS),$(ASAN_DIR)/dpac_eqn_$(e)_f32.o $(ASAN_DIR)/dpac_eqn_$(e)_f64.o)
+CLANG     ?= /opt/rocm/llvm/bin/clang
+SANRT     := $(dir $(firstword $(wildcard /opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so)))
+
+.PHONY: sanitize
+$(ASAN_DIR)/dpac_%.o: $(CSRC)/dpac_%.hip $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) $(ASAN_FLAGS) -c $< -o $@
+$(ASAN_DIR)/dpac_eqn_%_f32.o: $(CSRC)/dpac_eqn_%.hip $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) $(ASAN_FLAGS) -DDPAC_TU_DOUBLE=0 -c $< -o $@
+$(ASAN_DIR)/dpac_eqn_%_f64.o: $(CSRC)/dpac_eqn_%.hip $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) $(ASAN_FLAGS) -DDPAC_TU_DOUBLE=1 -c $< -o $@
+$(ASAN_DIR)/libdpac_asan.so: $(ASAN_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -fsanitize=address,undefined -shared-libsan -o $@ $(ASAN_OBJS)
+$(ASAN_DIR)/abi_sanitize: tests/abi_sanitize.c $(ASAN_DIR)/libdpac_asan.so include/dpac.h
+	$(CLANG) -g -O1 -fsanitize=address,undefined -shared-libsan -fno-omit-frame-pointer -Iinclude $< \
+	  -L$(ASAN_DIR) -ldpac_asan -Wl,-rpath,$(abspath $(ASAN_DIR)) -Wl,-rpath,$(SANRT) -o $@
+sanitize: $(ASAN_DIR)/abi_sanitize
+	ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
+	  $(ASAN_DIR)/abi_sanitize > $(ASAN_DIR)/abi_sanitize.log 2>&1; rc=$$?; tail -3 $(ASAN_DIR)/abi_sanitize.log; exit $$rc

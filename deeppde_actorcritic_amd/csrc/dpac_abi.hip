@@ -169,7 +169,12 @@ int launch(const OpArgs& a) {
   // 32-bit buffer descriptor whose offsets >= 2^31 mean "out of range".
   const int64_t esz = f64 ? 8 : 4;
   const int64_t width = a.eq.dim > a.eq.control_dim ? a.eq.dim : a.eq.control_dim;
-  if (a.B * width * ((int64_t)a.N + 1) * esz >= ((int64_t)1 << 31))
+  // B <= 2^31 and width <= 2^31 are checked before, so row_bytes cannot overflow; the step
+  // count is compared by division (B * width * (N + 1) * esz overflows int64 for huge N:
+  // found by the host UBSan run, tests/abi_sanitize.c)
+  if (width > (1 << 16)) return fail(DPAC_EINVAL, "dim %d / control_dim %d too large", a.eq.dim, a.eq.control_dim);
+  const int64_t limit = (int64_t)1 << 31, row_bytes = a.B * width * esz;
+  if (row_bytes >= limit || ((int64_t)a.N + 1) > (limit - 1) / row_bytes)
     return fail(DPAC_EINVAL, "batch too large for one launch: every [N+1][B][d] array must stay "
                 "below 2 GiB (B=%lld, N=%d, d=%d); split the batch over launches with "
                 "traj_offset", (long long)a.B, a.N, a.eq.dim);

@@ -165,6 +165,9 @@ __device__ __forceinline__ void mfma_rows16_km(const float* in, int K, int Nout,
 #ifndef DPAC_NN_KMS
 #define DPAC_NN_KMS 1  // 1: static-K (fully unrolled) k-major layers for the specialised K16
 #endif
+#ifndef DPAC_NN_SAVE_NT
+#define DPAC_NN_SAVE_NT 0
+#endif
 #ifndef DPAC_NN_PIN
 #define DPAC_NN_PIN 1  // sched_barrier after each k group of the static-K layers
 #endif
@@ -728,7 +731,11 @@ struct FwdEpi {
     store(0, row, col, valid, z, k);
   }
   __device__ __forceinline__ void store(int, int row, int col, bool valid, T z, const Col& k) const {
+#if DPAC_NN_SAVE_NT  // timing knob: non-temporal z saves
+    if (save && valid && row < rows_live) __builtin_nontemporal_store(z, save + row * save_stride + col);
+#else
     if (save && valid && row < rows_live) save[row * save_stride + col] = z;
+#endif
     T yv = bias ? z + k.bb : z;          // addmm(b, y, W) (solver.py:270)
     yv = k.sh + yv * k.s;                // addcmul(beta, y, gamma/sqrt(1+eps))
     if (hidden) yv = yv + fmax(yv, T(0));  // y + relu(y) (solver.py:269)

@@ -21,6 +21,17 @@
 // Included by dpac_kernels.h inside namespace dpac, after dpac_rollout_nn.h.
 
 constexpr int kNnBwdThreads = kNnThreads + 128;  // + stager + writer
+#ifndef DPAC_BWD2_GNT
+#define DPAC_BWD2_GNT 0  // timing knob: non-temporal G stores from the writer wave
+#endif
+#ifndef DPAC_BWD2_DMA_NT
+#define DPAC_BWD2_DMA_NT 0  // timing knob: the stager's LDS-DMA with the nt cache policy
+#endif
+#if DPAC_BWD2_DMA_NT
+#define DPAC_BWD2_DMA_POL " nt"
+#else
+#define DPAC_BWD2_DMA_POL ""
+#endif
 #ifndef DPAC_BWD2_ZREG
 #define DPAC_BWD2_ZREG 0  // timing knob: stage z through the stager's VGPRs instead of LDS-DMA
 #endif
@@ -56,7 +67,7 @@ __device__ __forceinline__ void wave_copy_lds(const void* src, uint32_t bytes, u
     const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds0 + k * 64 * SZ);
     int keep;
     if constexpr (SZ == 16)
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" DPAC_BWD2_DMA_POL "\n\ts_mov_b32 m0, %0"
                    : "=&s"(keep) : "v"(gp), "s"(m0) : "memory");
     else
       asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -170,10 +181,17 @@ __device__ __forceinline__ void write_G_rows(const T* img, int per_row, T* G, in
     asm volatile("" ::"v"(v0), "v"(v1), "v"(v2), "v"(v3));
     continue;
 #endif
+#if DPAC_BWD2_GNT  // timing knob: non-temporal G stores
+    if (act && ra < rows_live) __builtin_nontemporal_store(v0, reinterpret_cast<vec*>(G + ra * gtot + goff + q * V));
+    if (act && rb1 < rows_live) __builtin_nontemporal_store(v1, reinterpret_cast<vec*>(G + rb1 * gtot + goff + q * V));
+    if (act && rc < rows_live) __builtin_nontemporal_store(v2, reinterpret_cast<vec*>(G + rc * gtot + goff + q * V));
+    if (act && rd < rows_live) __builtin_nontemporal_store(v3, reinterpret_cast<vec*>(G + rd * gtot + goff + q * V));
+#else
     if (act && ra < rows_live) *reinterpret_cast<vec*>(G + ra * gtot + goff + q * V) = v0;
     if (act && rb1 < rows_live) *reinterpret_cast<vec*>(G + rb1 * gtot + goff + q * V) = v1;
     if (act && rc < rows_live) *reinterpret_cast<vec*>(G + rc * gtot + goff + q * V) = v2;
     if (act && rd < rows_live) *reinterpret_cast<vec*>(G + rd * gtot + goff + q * V) = v3;
+#endif
   }
 }
 
