@@ -292,7 +292,7 @@ def main():
                    "scheme": args.scheme, "parallelism": f"dp{world} (trajectory shards)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": tsrc, "kernel": "dpac::k_rollout",
+                     "traffic_source": tsrc, "kernel": "dpac::k_rollout_staged",
                      "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": per_launch_ms},
     }
     if not args.no_variants:

@@ -443,6 +443,237 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
 }
 
 // ---------------------------------------------------------------------------
+// k_rollout with the increments staged through LDS by a loader wavefront.
+//
+// Why: gfx950 counts a wave's vector loads and stores in ONE in-order vmcnt, so in
+// k_rollout the wait for step t's dw also waits for every x / dt / coef store issued
+// before that load.  With HBM-cold data (measured, 5 rotating sets, B = 4096): loads
+// alone 24.9 us, stores alone 26.8 us, both 38.5 us — the coupling, not bandwidth,
+// costs the difference (profiles/r02_rollout_cold_ablations.txt).
+// Here a workgroup is CW = 4 compute wavefronts (16 trajectories at P = 16) plus one
+// LOADER wavefront that copies the workgroup's dw rows of each step (one contiguous
+// row block in the step-major layout) into an RS-step LDS ring with global_load_lds,
+// CH steps ahead of use; the compute wavefronts read dw from LDS and only store.  The
+// loader's vmcnt holds only its DMA; the compute waves' holds only stores, which no
+// one waits for.  Hand-off through LDS counters: `ready` (steps landed, loader) and
+// `done[w]` (steps consumed, per compute wave), polled with s_sleep; the loader stays
+// at most RS steps ahead.  Arithmetic per step is k_rollout's (bitwise the same).
+// ---------------------------------------------------------------------------
+#ifndef DPAC_ST_CHUNKS
+#define DPAC_ST_CHUNKS 4  // hand-off chunks in the LDS ring
+#endif
+constexpr int kStCW = 4;   // compute wavefronts per workgroup
+constexpr int kStCH = 16;  // steps per hand-off chunk
+template <typename T, int D, int P>
+struct StagedPlan {
+  static constexpr int TPW = kStCW * (64 / P);                                   // trajectories per workgroup
+  static constexpr int SLOT = TPW * D * (int)sizeof(T);                          // bytes of one step's rows
+  static constexpr int PIECES = (SLOT + 1023) / 1024;                            // 1 KB DMA instructions per step
+  static constexpr int SLOT_LDS = (SLOT + 16 + 1023) / 1024 * 1024;              // + a zero pad no DMA writes
+  static constexpr int PADOFF = SLOT_LDS - 16;                                   // where empty lanes read 0
+  // ring depth (steps): the loader publishes a chunk once the next one is issued, so it
+  // needs >= 2 chunks; 4 keep it far enough ahead that the compute waves never wait
+  // (measured at B = 4096, cold: 4 chunks 29.3 us, 2 chunks 41.6, k_rollout 38.3); where 4
+  // chunks do not fit in 128 KB (float64 at d = 20) k_rollout runs instead
+  static constexpr int RS = DPAC_ST_CHUNKS * kStCH;
+  static constexpr bool kOk = P >= 4 && RS * SLOT_LDS <= 128 * 1024 && kStCH * PIECES <= 62;
+};
+
+template <class Fn, int... S>
+__device__ __forceinline__ void unroll_phases(Fn& fn, std::integer_sequence<int, S...>) {
+  (fn(Phase<S>{}), ...);
+}
+
+__device__ __forceinline__ int lds_load_relaxed(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_relaxed(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <typename T, class E, int D, int SCHEME, int OUT, int KB>
+__global__ __launch_bounds__(64 * (kStCW + 1)) void k_rollout_staged(const E eq, const DevConsts<T> c,
+                                                                      const RolloutArgs<T> a) {
+  constexpr int P = E::kP, M = E::M, MC = E::MC;
+  using PL = StagedPlan<T, D, P>;
+  constexpr int TPW = PL::TPW, RS = PL::RS, PIECES = PL::PIECES, SLOT_LDS = PL::SLOT_LDS;
+  constexpr bool COST = (OUT & kOutCost) != 0, WANT_U = (OUT & kOutU) != 0;
+  constexpr int F = P < kStCH ? P : kStCH;
+  static_assert(kStCH % F == 0 && (F & (F - 1)) == 0, "flush phase fixed per unrolled body");
+  using TR = Transition<T, E, SCHEME>;
+  __shared__ __attribute__((aligned(16))) unsigned char s_ring[RS * SLOT_LDS];
+  __shared__ int s_ready, s_done[kStCW];
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / 64), lane = (int)threadIdx.x % 64;
+  const int64_t row0 = xcd_block(blockIdx.x, gridDim.x) * TPW;
+  const int N = a.N;
+  if (threadIdx.x == 0) {
+    s_ready = 0;
+#pragma unroll
+    for (int w = 0; w < kStCW; ++w) s_done[w] = 0;
+  }
+  if (threadIdx.x < RS * 4)  // the zero pads (lanes that own no component read them)
+    reinterpret_cast<uint32_t*>(s_ring + (threadIdx.x / 4) * SLOT_LDS + PL::PADOFF)[threadIdx.x % 4] = 0u;
+  __syncthreads();
+
+  if (wave == kStCW) {  // ---- loader: dw rows of steps t -> ring slot t % RS ----
+    const int64_t rows_live = (a.B - row0) < TPW ? (a.B - row0) : TPW;
+    const uint32_t bytes = (uint32_t)(rows_live * D * (int64_t)sizeof(T));
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)s_ring;
+    const char* base = (const char*)(a.dw + row0 * D);
+    const int64_t step_bytes = a.B * D * (int64_t)sizeof(T);
+    for (int c0 = 0; c0 < N; c0 += kStCH) {
+      // the slots of this chunk were last read at steps c0 + s - RS: wait for every consumer
+      const int need = c0 + kStCH - RS;
+      if (need > 0) {
+        for (;;) {
+          int mn = lds_load_relaxed(&s_done[0]);
+#pragma unroll
+          for (int w = 1; w < kStCW; ++w) mn = min(mn, lds_load_relaxed(&s_done[w]));
+          if (mn >= need) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int s = 0; s < kStCH; ++s) {
+        const int t = c0 + s < N ? c0 + s : N - 1;  // past the end: re-copy the last step (unused)
+        const char* src = base + t * step_bytes;
+        const uint32_t slot = lds0 + (uint32_t)((t % RS) * SLOT_LDS);
+#pragma unroll
+        for (int k = 0; k < PIECES; ++k) {
+          const uint32_t off = (uint32_t)((k * 64 + lane) * 16);
+          const char* gp = src + (off < bytes ? off : 0u);  // lane 0 past the rows re-reads row 0
+          const uint32_t m0 = __builtin_amdgcn_readfirstlane(slot + (uint32_t)(k * 1024));
+          // lanes past the rows write nothing (the zero pad stays zero); lane 0 always issues,
+          // so every instruction counts in vmcnt (it lands at k*1024, never on the pad)
+          if (off < bytes || lane == 0) {
+            int keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(gp), "s"(m0) : "memory");
+          }
+        }
+      }
+      // the previous chunk has landed once only this chunk's copies are outstanding
+      if (c0 > 0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStCH * PIECES) : "memory");
+        if (lane == 0) lds_store_relaxed(&s_ready, c0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) lds_store_relaxed(&s_ready, N);
+    return;
+  }
+
+  // ---- compute wavefronts: k_rollout's time loop with dw from the ring ----
+  const LaneCoord<P> lc(a.B, lane, row0 + wave * (64 / P));
+  const int gl = wave * (64 / P) + lane / P;  // trajectory within the workgroup
+  const Own<D, P> own(lc.p);
+  const Own<E::CDIM, P> ownu(lc.p);
+  const BufSlab<T, D, P> sx(own, lc.b, lc.live);
+  const BufSlab<T, E::CDIM, P> su(ownu, lc.b, lc.live);
+  const uint32_t slab = (uint32_t)(a.B * D * sizeof(T));
+  const uint32_t slab_u = (uint32_t)(a.B * E::CDIM * sizeof(T));
+  const uint32_t row_bytes = (uint32_t)(N * sizeof(T));
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(a.x, slab * (uint32_t)(N + 1));
+  const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(a.u, WANT_U ? slab_u * (uint32_t)N : 0u);
+  const __amdgpu_buffer_rsrc_t rs_dt = make_rsrc(a.dt, (uint32_t)a.B * row_bytes);
+  const __amdgpu_buffer_rsrc_t rs_cf = make_rsrc(a.coef, (uint32_t)a.B * row_bytes);
+  const T* ring = reinterpret_cast<const T*>(s_ring);
+  const int lds_e = gl * D + lc.p * M;  // element offset of this lane's components in a slot
+  // full-or-empty lanes: one vector LDS read per step, empty lanes aimed at the zero pad
+  constexpr bool kVecRead = Own<D, P>::kFull && (M * sizeof(T) == 8 || M * sizeof(T) == 16);
+  const uint32_t lane_off = own.active() ? (uint32_t)(lds_e * (int)sizeof(T)) : (uint32_t)PL::PADOFF;
+  T keep = 0;
+  auto flush = [&](int t_last, int count) {
+    const uint32_t off = (lc.live && lc.p < count)
+                             ? (uint32_t)((lc.b * N + t_last - lc.p) * (int64_t)sizeof(T)) : kOOB;
+    buf_store_scalar<T>(rs_dt, off, fabs(keep));
+    buf_store_scalar<T>(rs_cf, off, keep > T(0) ? T(1) : T(0));
+  };
+  T x[M];
+  sx.load(make_rsrc(a.x0, slab), x);
+  sx.store(rs_x, x);
+  T r = TR::kRadius ? dsqrt(Lanes<P>::sum(sumsq(x))) : T(0);
+  Flags fl = SCHEME == DPAC_SCHEME_ADAPTIVE ? region(r, c) : Flags{true, false};
+  T disc = 1, y = 0;
+  // slot_bytes: (t % RS) * SLOT_LDS, formed once per chunk plus a compile-time step offset
+  auto read_dw_at = [&](int t, uint32_t slot_bytes, T (&dwv)[M]) {  // components past d read 0
+    if constexpr (kVecRead) {
+      typedef T vec __attribute__((ext_vector_type(M)));
+      const vec v = *reinterpret_cast<const vec*>(s_ring + slot_bytes + lane_off);
+#pragma unroll
+      for (int m = 0; m < M; ++m) dwv[m] = v[m];
+    } else {
+      const T* slot = ring + (t % RS) * (SLOT_LDS / (int)sizeof(T)) + lds_e;
+#pragma unroll
+      for (int m = 0; m < M; ++m) dwv[m] = own.valid(m) ? slot[m] : T(0);
+    }
+  };
+  auto read_dw = [&](int t, T (&dwv)[M]) { read_dw_at(t, (uint32_t)((t % RS) * SLOT_LDS), dwv); };
+  auto body = [&](int t, const T (&dwv)[M], auto phase) {
+    T u[MC];
+    eq.u_true(x, r, u);
+    TR tr;
+    tr.run(eq, c, x, u, dwv, fl, r);
+    const T cf = tr.coef ? T(1) : T(0);
+    if constexpr (COST) {
+      const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(x, u)));
+      y += cost_increment(a.cost_order, w, cf, tr.dt, disc);
+      disc = disc * disc_factor(tr.dt, cf, c);
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) x[m] = tr.coef ? tr.xt[m] : x[m];
+    if constexpr (TR::kRadius) r = tr.coef ? tr.rt : r;
+    fl = tr.next;
+    sx.template store<DPAC_ROLLOUT_X_AUX>(rs_x, x, (uint32_t)(t + 1) * slab);
+    if constexpr (WANT_U) su.store(rs_u, u, (uint32_t)t * slab_u);
+    constexpr int PH = decltype(phase)::value;
+    keep = group_shift_in<P>(keep, tr.coef ? tr.dt : -tr.dt, lc.p == 0);
+    if constexpr (PH >= 0) {
+      if constexpr (PH % F == F - 1) flush(t, F);
+    } else if ((t & (F - 1)) == F - 1) {
+      flush(t, F);
+    }
+  };
+  for (int c0 = 0; c0 < N; c0 += kStCH) {
+    const int want = c0 + kStCH < N ? c0 + kStCH : N;
+    while (lds_load_relaxed(&s_ready) < want) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+    if (c0 + kStCH <= N) {
+      // RS is a multiple of kStCH: the chunk's slots are contiguous from cb
+      const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane((c0 % RS) * SLOT_LDS);
+      T nxt[M];
+      read_dw_at(c0, cb, nxt);
+      auto one = [&](auto sidx) {
+        constexpr int S = decltype(sidx)::value;
+        T cur[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) cur[m] = nxt[m];
+        if constexpr (S + 1 < kStCH) read_dw_at(c0 + S + 1, cb + (uint32_t)((S + 1) * SLOT_LDS), nxt);
+        body(c0 + S, cur, Phase<S>{});
+      };
+      unroll_phases(one, std::make_integer_sequence<int, kStCH>{});
+    } else {
+      for (int t = c0; t < N; ++t) {
+        T cur[M];
+        read_dw(t, cur);
+        body(t, cur, Phase<-1>{});
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) lds_store_relaxed(&s_done[wave], want);
+  }
+  const int rem = N & (F - 1);
+  if (rem) flush(N - 1, rem);
+  if constexpr (COST) {
+    if (lc.live && lc.p == 0) {
+      a.y[lc.b] = y;
+      a.disc[lc.b] = disc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Flag initialisation (adaptive: equation.py:78-82; naive: np.ones, :52)
 // ---------------------------------------------------------------------------
 template <typename T, class E, int D, int SCHEME>
@@ -821,6 +1052,13 @@ inline uint32_t bptt_lds(uint32_t need, uint32_t cap) {
   return v > need ? (v < cap ? v : cap) : need;
 }
 
+// Analytic rollout with dw staged through LDS (k_rollout_staged, default) or read directly
+// (k_rollout): DPAC_ROLLOUT_STAGED=0 forces the latter (tests compare the two bit for bit).
+inline bool rollout_staged() {
+  const char* e = getenv("DPAC_ROLLOUT_STAGED");  // read per launch
+  return !(e && e[0] == '0');
+}
+
 inline int nn_tile_rows() {
   const char* e = getenv("DPAC_NN_TILE");  // read per launch: tests switch it in-process
   const int v = e ? atoi(e) : 0;
@@ -852,6 +1090,25 @@ int run_op(const OpArgs& a) {
       const bool philox = a.dw == nullptr, cost = a.y != nullptr;
       constexpr int KB = rollout_kb(ring_kb((int)sizeof(DwFrame<T, E::M>), DPAC_RING_VGPRS, DPAC_ROLLOUT_KB_CAP), E::kP);
       const int out = (cost ? kOutCost : 0) | (a.u_out ? kOutU : 0);
+      using SP = StagedPlan<T, D, E::kP>;
+      if constexpr (SP::kOk) {
+        if (!philox && rollout_staged()) {  // dw through the loader wave's LDS ring
+          const dim3 sgrid((unsigned)((a.B + SP::TPW - 1) / SP::TPW)), sblock(64 * (kStCW + 1));
+#define DPAC_ROLL_ST(SCH, OUT) \
+  hipLaunchKernelGGL((k_rollout_staged<T, E, D, SCH, OUT, KB>), sgrid, sblock, 0, s, eq, c, r)
+#define DPAC_ROLL_ST_SCH(SCH)                                  \
+  switch (out) {                                               \
+    case 0: DPAC_ROLL_ST(SCH, 0); break;                       \
+    case kOutCost: DPAC_ROLL_ST(SCH, kOutCost); break;         \
+    case kOutU: DPAC_ROLL_ST(SCH, kOutU); break;               \
+    default: DPAC_ROLL_ST(SCH, kOutCost | kOutU); break;       \
+  }
+          if (adaptive) { DPAC_ROLL_ST_SCH(DPAC_SCHEME_ADAPTIVE) } else { DPAC_ROLL_ST_SCH(DPAC_SCHEME_NAIVE) }
+#undef DPAC_ROLL_ST_SCH
+#undef DPAC_ROLL_ST
+          break;
+        }
+      }
 #define DPAC_ROLL(SCH, PH, OUT) \
   hipLaunchKernelGGL((k_rollout<T, E, D, SCH, PH, OUT, KB>), grid, block, 0, s, eq, c, r)
 #define DPAC_ROLL_PH(SCH, PH)                              \

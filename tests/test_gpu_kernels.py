@@ -274,3 +274,35 @@ def test_odd_batch_sizes():
         x, dt, coef, *_ = ops.rollout_analytic(ep.params(), 1, dev(x0), native_dw(dw), 0.2, 12)
         np.testing.assert_array_equal(coef.cpu().numpy(), cr.numpy())
         assert rel_close(x.permute(1, 2, 0).cpu(), xr, 1e-12)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("scheme", ["adaptive", "naive"])
+@pytest.mark.parametrize("name,d,B,N", [("LQR", 20, 300, 200), ("LQR", 5, 37, 13), ("EKN", 20, 65, 7),
+                                        ("LQR_var", 10, 33, 101), ("LQR", 4, 1, 40), ("VDP", 20, 70, 30)])
+def test_staged_rollout_bitwise(name, d, B, N, scheme, dtype):
+    """k_rollout_staged (dw copied into an LDS ring by a loader wavefront, the compute
+    wavefronts only store) gives bitwise the results of k_rollout, which loads dw itself:
+    full and partial hand-off chunks, partial workgroups, the u and cost outputs, both
+    dtypes (VDP's one-lane groups always take k_rollout)."""
+    cfg = eqn_config(name, d, T=0.2, N=N)
+    eqp = pe(cfg).params()
+    sch = SCHEMES[scheme]
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=3, dtype=dtype, device=DEV)
+    out = {}
+    old = os.environ.get("DPAC_ROLLOUT_STAGED")
+    try:
+        for k in ("0", "1"):
+            os.environ["DPAC_ROLLOUT_STAGED"] = k
+            out[k] = [ops.rollout_analytic(eqp, sch, x0, dw, 0.2, N, want_u=wu, cost_order=co)
+                      for wu, co in ((False, None), (True, _lib.COST_ACTOR))]
+    finally:
+        if old is None:
+            os.environ.pop("DPAC_ROLLOUT_STAGED", None)
+        else:
+            os.environ["DPAC_ROLLOUT_STAGED"] = old
+    for a, b in zip(out["0"], out["1"]):
+        for s, t in zip(a, b):
+            assert (s is None) == (t is None)
+            if s is not None:
+                assert torch.equal(s, t)

@@ -4,7 +4,7 @@
     python tools/collect_profiles.py r01
 
 * profiles/<tag>_kernel_stats.csv  — rocprofv3 --kernel-trace --stats summary
-* profiles/<tag>_pmc_rollout.json  — FETCH_SIZE / WRITE_SIZE per dpac::k_rollout launch,
+* profiles/<tag>_pmc_rollout.json  — FETCH_SIZE / WRITE_SIZE per dpac::k_rollout_staged launch,
   corrected as MI355X_MICROARCH.md §HBM prescribes (separate passes; counters in KiB;
   gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream -> x2)
 * profiles/pmc_traffic.json        — the per-launch HBM bytes bench.py reports as
@@ -54,7 +54,8 @@ def main(tag):
         print("no PMC passes found")
         return
     # canonical rollout: f32, LQR d=20 (16 lanes/trajectory), adaptive, dw from HBM, no cost/u outputs
-    key_kernel = "k_rollout<float, dpac::EqLQR<float, 20, 16>, 20, 1, false, 0,"
+    # (the LDS-staged kernel k_rollout_staged; k_rollout takes Philox / unstaged shapes)
+    key_kernel = "k_rollout_staged<float, dpac::EqLQR<float, 20, 16>, 20, 1, 0,"
     fetch_kib, nf, row = counter_mean(f, key_kernel, "FETCH_SIZE")
     write_kib, nw, _ = counter_mean(w, key_kernel, "WRITE_SIZE")
     fetch_b = fetch_kib * 1024 * 2  # gfx950: FETCH_SIZE counts 64 B per 128-B request
