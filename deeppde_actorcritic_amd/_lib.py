@@ -93,6 +93,12 @@ SIGNATURES = {
     "dpac_rollout_nn_bwd": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp),
                             ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), _P, _P,
                             _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "dpac_rollout_nn_mask_tile_bytes": [ctypes.POINTER(Mlp)],
+    "dpac_rollout_nn_fwd_masked": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp), _P, _P, _P, _P,
+                                   _P, _P, _I32, _P, _P, _P, _P, _P, _P, ctypes.POINTER(_I32), _P],
+    "dpac_rollout_nn_bwd_masked": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp),
+                                   ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), _P, _P,
+                                   _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "dpac_mlp_rows_fwd": [_I32, _I64, ctypes.POINTER(Mlp), _P, _I64, _P, _P, _P],
     "dpac_mlp_rows_bwd": [_I32, _I64, ctypes.POINTER(Mlp), ctypes.POINTER(ctypes.c_void_p),
                           ctypes.POINTER(ctypes.c_void_p), _P, _P, _P, _P, _P],

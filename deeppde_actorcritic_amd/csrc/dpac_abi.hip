@@ -363,12 +363,29 @@ int dpac_rollout_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype, i
   return launch(a);
 }
 
+int32_t dpac_rollout_nn_mask_tile_bytes(const dpac_mlp* actor) {
+  if (!actor || actor->n_hidden < 1 || actor->n_hidden > DPAC_MLP_MAX_HIDDEN) return 0;
+  return nn_mask_tile_bytes(actor->n_hidden);
+}
+
 int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
                         int64_t num_sample, int32_t num_steps, double total_time,
                         const dpac_mlp* actor, const void* x0, const void* dw, void* x,
                         void* dt, void* coef, void* u, int32_t cost_order, void* y,
                         void* disc, void* save_z, int32_t* save_flag, void* save_disc,
                         void* stream) {
+  return dpac_rollout_nn_fwd_masked(eq, scheme, dtype, num_sample, num_steps, total_time, actor, x0, dw, x,
+                                    dt, coef, u, cost_order, y, disc, save_z, save_flag, save_disc, nullptr,
+                                    nullptr, stream);
+}
+
+int dpac_rollout_nn_fwd_masked(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                               int64_t num_sample, int32_t num_steps, double total_time,
+                               const dpac_mlp* actor, const void* x0, const void* dw, void* x,
+                               void* dt, void* coef, void* u, int32_t cost_order, void* y,
+                               void* disc, void* save_z, int32_t* save_flag, void* save_disc,
+                               uint8_t* save_mask, int32_t* mask_written, void* stream) {
+  if (mask_written) *mask_written = 0;
   if (int e = check_common(eq, dtype, num_sample)) return e;
   if (int e = check_time(scheme, num_steps, total_time)) return e;
   if (int e = check_mlp(eq, actor)) return e;
@@ -389,6 +406,8 @@ int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
   a.x0 = x0; a.dw = dw; a.mlp = *actor;
   a.x_out = x; a.dt = dt; a.coef = coef; a.u_out = u; a.cost_order = cost_order; a.y = y;
   a.disc = disc; a.save_z = save_z; a.save_flag = save_flag; a.save_disc = save_disc;
+  if (save_mask && nsave != 3) return fail(DPAC_EINVAL, "save_mask needs the other backward saves");
+  a.save_mask = save_mask; a.mask_written = mask_written;
   a.stream = (hipStream_t)stream;
   return launch(a);
 }
@@ -401,6 +420,20 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
                         const int32_t* save_flag, const void* save_disc, const void* g_xN,
                         const void* g_disc, const void* g_y, void* G, void* g_x0,
                         void* stream) {
+  return dpac_rollout_nn_bwd_masked(eq, scheme, dtype, num_sample, num_steps, total_time, actor, weight_t,
+                                    weight_t_km, x, u, dw, save_z, save_flag, save_disc, nullptr, g_xN,
+                                    g_disc, g_y, G, g_x0, stream);
+}
+
+int dpac_rollout_nn_bwd_masked(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                               int64_t num_sample, int32_t num_steps, double total_time,
+                               const dpac_mlp* actor, const void* const* weight_t,
+                               const void* const* weight_t_km, const void* x,
+                               const void* u, const void* dw, const void* save_z,
+                               const int32_t* save_flag, const void* save_disc,
+                               const uint8_t* save_mask, const void* g_xN,
+                               const void* g_disc, const void* g_y, void* G, void* g_x0,
+                               void* stream) {
   if (int e = check_common(eq, dtype, num_sample)) return e;
   if (int e = check_time(scheme, num_steps, total_time)) return e;
   if (int e = check_mlp(eq, actor)) return e;
@@ -424,6 +457,7 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
   a.x = x; a.u = u; a.dw = dw; a.save_z = const_cast<void*>(save_z);
   a.save_flag = const_cast<int32_t*>(save_flag); a.save_disc = const_cast<void*>(save_disc);
   a.g_x_out = g_xN; a.g_disc_out = g_disc; a.g_y_out = g_y; a.g_G = G; a.g_x = g_x0;
+  a.mask_in = save_mask;
   a.stream = (hipStream_t)stream;
   return launch(a);
 }

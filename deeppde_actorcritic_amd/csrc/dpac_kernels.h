@@ -34,6 +34,10 @@ enum Op : int {
   OP_ROLLOUT_NN_BWD,
 };
 
+// Bytes per 16-row tile of the sign-bit mask (FwdEpiM): 13 16-column tiles per hidden layer
+// (the fast path's 193..208-wide layers), 64 bytes each.
+inline int nn_mask_tile_bytes(int n_hidden) { return 13 * 64 * n_hidden; }
+
 // Everything any op may need; unused fields are ignored.
 struct OpArgs {
   int op;
@@ -52,6 +56,9 @@ struct OpArgs {
   dpac_mlp mlp;                  // OP_ROLLOUT_NN: the actor MLP
   void *save_z, *save_disc;      // OP_ROLLOUT_NN: optional backward saves
   int32_t* save_flag;
+  uint8_t* save_mask;            // OP_ROLLOUT_NN: optional sign-bit mask (fast path only)
+  int32_t* mask_written;         // OP_ROLLOUT_NN: host flag, 1 if the mask was written
+  const uint8_t* mask_in;        // OP_ROLLOUT_NN_BWD: the forward's mask, or null
   const void* mlp_wt[DPAC_MLP_MAX_HIDDEN + 1];  // OP_ROLLOUT_NN_BWD: (W_i diag s_{i+1})^T
   hipStream_t stream;
 };
@@ -1200,11 +1207,13 @@ int run_op(const OpArgs& a) {
       }
       // the fast path serves k_rollout_nn_bwd2 (the generic k_rollout_nn_bwd ignores it)
       r.fast = nn_fast_host<T>(m.L, m.width, (const void* const*)r.wtkm, m.width[m.L + 1], m.width[0]);
+      r.mask = r.fast ? a.mask_in : nullptr;
+      r.mb = nn_mask_tile_bytes(m.L);
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
       if (bptt_kernel() == 2) {
         int wsum = 0;
         for (int i = 0; i <= m.L + 1; ++i) wsum += m.width[i];
-        const BwdPlan<T, D, E::CDIM> pl(wsum, m.ztot, true);
+        const BwdPlan<T, D, E::CDIM> pl(wsum, m.ztot, true, r.mask ? r.mb : 0);
         const uint32_t lds = bptt_lds(pl.total, BwdPlan<T, D, E::CDIM>::kMaxDyn);
         const dim3 nb2(kNnBwdThreads);
 #define DPAC_BWD2(SCH, ZS)                                                                          \
@@ -1215,6 +1224,17 @@ int run_op(const OpArgs& a) {
       return (int)e;                                                                                \
     hipLaunchKernelGGL(kfn, ngrid, nb2, lds, s, eq, c, m, r);                                       \
   }
+        if constexpr (kFastOk) {
+          if (r.mask) {  // the sign-bit mask instead of z (fast path)
+            auto kfn = adaptive ? k_rollout_nn_bwd2<T, E, D, DPAC_SCHEME_ADAPTIVE, false, true, true>
+                                : k_rollout_nn_bwd2<T, E, D, DPAC_SCHEME_NAIVE, false, true, true>;
+            if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
+              return (int)e;
+            hipLaunchKernelGGL(kfn, ngrid, nb2, lds, s, eq, c, m, r);
+            break;
+          }
+        }
         if (adaptive) {
           if (pl.zst) DPAC_BWD2(DPAC_SCHEME_ADAPTIVE, true) else DPAC_BWD2(DPAC_SCHEME_ADAPTIVE, false)
         } else {
@@ -1252,6 +1272,8 @@ int run_op(const OpArgs& a) {
       r.x = (T*)a.x_out; r.dt = (T*)a.dt; r.coef = (T*)a.coef; r.u = (T*)a.u_out;
       r.y = (T*)a.y; r.disc = (T*)a.disc;
       r.save_z = (T*)a.save_z; r.save_disc = (T*)a.save_disc; r.save_flag = a.save_flag;
+      r.save_mask = nullptr;
+      r.mb = nn_mask_tile_bytes(m.L);
       const bool cost = a.y != nullptr;
       if constexpr (std::is_same<T, float>::value) {
         // 4-row MFMA blocks (dpac_rollout_nn4.h) where the 16-row tiles would leave
@@ -1276,9 +1298,15 @@ int run_op(const OpArgs& a) {
         }
       }
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
+      if (m.fast && a.save_mask && a.save_z) {  // the 16-row fast path writes the sign bits
+        r.save_mask = a.save_mask;
+        if (a.mask_written) *a.mask_written = 1;
+      }
 #define DPAC_ROLL_NN(SCH, CO)                                                                                   \
   do {                                                                                                          \
-    if (m.fast) hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1, kFastOk>), ngrid, nblock, 0, s, eq, c, m, r); \
+    if (m.fast && r.save_mask)                                                                                  \
+      hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1, kFastOk, kFastOk>), ngrid, nblock, 0, s, eq, c, m, r); \
+    else if (m.fast) hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1, kFastOk>), ngrid, nblock, 0, s, eq, c, m, r); \
     else hipLaunchKernelGGL((k_rollout_nn<T, E, D, SCH, CO, 1, false>), ngrid, nblock, 0, s, eq, c, m, r);      \
   } while (0)
       if (adaptive) {

@@ -84,6 +84,9 @@ struct NnRolloutArgs {
   const T *x0, *dw;
   T *x, *dt, *coef, *u, *y, *disc, *save_z, *save_disc;
   int32_t* save_flag;
+  uint8_t* save_mask;   // optional (fast path only): the hidden activations' sign bits,
+                        // [N][ceil(B/16)][mb] bytes (FwdEpiM's layout per 16-row tile)
+  int mb;               // mask bytes per 16-row tile
 };
 
 // out[16 x Nout] = in[16 x K] @ W[K x Nout] for the workgroup's 16 rows, this
@@ -743,6 +746,29 @@ struct FwdEpi {
   }
 };
 
+// FwdEpi that also records the sign of every hidden BN output (the only thing the BPTT
+// needs of z: the activation factor 1 + [y > 0]) in the accumulator's own layout: per
+// 16-row tile, hidden layer l, column c, row r: bit r % 4 of byte [13 l + c / 16][16 (r / 4)
+// + c % 16] (a 16x16 accumulator keeps a lane's four slots in one row quad and column, so
+// the byte is the lane's).  Each lane ORs its four slots' comparisons into one byte; a
+// 64-byte coalesced store per column tile, no cross-lane step.
+template <typename T>
+struct FwdEpiM : FwdEpi<T> {
+  uint8_t* mask;  // this step's mask tile of the workgroup's rows at this layer's offset
+  uint32_t nib;   // the four slots' bits of the current column tile
+  __device__ __forceinline__ void store(int i, int row, int col, bool valid, T z, const typename FwdEpi<T>::Col& k) {
+    if (this->save && valid && row < this->rows_live) this->save[row * this->save_stride + col] = z;
+    T yv = this->bias ? z + k.bb : z;
+    yv = k.sh + yv * k.s;
+    // the forward's own comparison, so the BPTT's activation factor is bitwise the z-based one
+    nib = (i == 0 ? 0u : nib) | ((valid && yv > T(0)) ? 1u << i : 0u);
+    yv = yv + fmax(yv, T(0));  // hidden layers only
+    this->out[row * kNnLd + col] = valid ? yv : T(0);
+    // dead rows' bits are written too and never read
+    if (i == 3) mask[(col >> 4) * 64 + 16 * (row >> 2) + (col & 15)] = (uint8_t)nib;
+  }
+};
+
 // Backward epilogue of a dense layer's input-gradient product g = G_{l+1} @ (W_l diag s_{l+1})^T:
 // for l >= 1 multiply by the activation factor 1 + [y_l > 0] of the forward step
 // (y_l = BN_l(z_l), z_l saved by the forward), then store the gradient entering
@@ -826,6 +852,8 @@ struct NnBackArgs {
   int goff[DPAC_MLP_MAX_HIDDEN + 2];     // column offset of G_i in a G row
   int gtot;
   int fast;  // the actor-shape fast path applies to the transposed chain (nn_fast_host)
+  const uint8_t* mask;  // optional (fast path): the forward's sign bits, [N][ceil(B/16)][mb]
+  int mb;
 };
 
 // The actor's BPTT through a fused NN rollout, as one launch: the reverse time
@@ -945,7 +973,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd(const E eq, const
   if (a.g_x0 && live) own.store(a.g_x0 + lc.b * D, lam);
 }
 
-template <typename T, class E, int D, int SCHEME, bool COST, int KB, bool FAST>
+template <typename T, class E, int D, int SCHEME, bool COST, int KB, bool FAST, bool MASK = false>
 __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const DevConsts<T> c,
                                                           const NnMlp<T> mlp,
                                                           const NnRolloutArgs<T> a) {
@@ -1026,7 +1054,19 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
                     a.save_z ? a.save_z + ((int64_t)t * a.B + row0) * mlp.ztot + mlp.zoff[l + 1] : nullptr,
                     mlp.ztot, rows_live};
       if constexpr (FAST) {
-        if (l == 0) {
+        if (MASK && l < L) {  // hidden output with its sign bits
+          FwdEpiM<T> epm;
+          static_cast<FwdEpi<T>&>(epm) = epi;
+          epm.mask = a.save_mask + ((int64_t)t * ((a.B + 15) >> 4) + (row0 >> 4)) * a.mb + 13 * 64 * l;
+          epm.nib = 0;
+          if (l == 0) {
+            if (L >= 2) load_wide_pre(pre, mlp.wkm[1], mlp.width[1], mlp.width[2], wave, lane);
+            nn_layer_narrow_in(in, mlp.width[0], mlp.width[1], res_in, wave, lane, epm);
+          } else {
+            nn_layer_wide(in, mlp.width[l + 1], mlp.wkm[l], pre, wave, lane, epm);
+            if (l + 1 < L) load_wide_pre(pre, mlp.wkm[l + 1], mlp.width[l + 1], mlp.width[l + 2], wave, lane);
+          }
+        } else if (l == 0) {
           if (L >= 2) load_wide_pre(pre, mlp.wkm[1], mlp.width[1], mlp.width[2], wave, lane);
           nn_layer_narrow_in(in, mlp.width[0], mlp.width[1], res_in, wave, lane, epi,
                              [&](int pt) { NN_MARK(t, pt); });

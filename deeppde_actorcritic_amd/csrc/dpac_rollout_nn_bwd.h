@@ -91,11 +91,18 @@ struct BwdPlan {
   static constexpr uint32_t kPar = kFlag + 256;  // one parity buffer of step inputs
   uint32_t bn, in, z, zpar, total;
   bool zst;
-  // widths sum = Σ_i width[i] (the BN image: scale then shift); ztot = Σ_{i>=1} width[i]
-  __host__ __device__ BwdPlan(int wsum, int ztot, bool want_z) {
+  // widths sum = Σ_i width[i] (the BN image: scale then shift); ztot = Σ_{i>=1} width[i];
+  // mask_tile_bytes > 0: the parity buffers hold the sign-bit mask tile instead of z
+  __host__ __device__ BwdPlan(int wsum, int ztot, bool want_z, int mask_tile_bytes = 0) {
     bn = 0;
     in = round_up(2u * (uint32_t)wsum * sizeof(T), 16);
     z = in + 2 * kPar;
+    if (mask_tile_bytes > 0) {
+      zst = false;
+      zpar = round_up((uint32_t)mask_tile_bytes, 1024);
+      total = z + 2 * zpar;
+      return;
+    }
     zpar = round_up((uint32_t)(kNnRows * ztot) * sizeof(T), 1024);
     zst = want_z && ((ztot * sizeof(T)) % 16 == 0) && z + 2 * zpar <= kMaxDyn;
     total = zst ? z + 2 * zpar : z;
@@ -158,6 +165,32 @@ struct BwdEpiL {
   }
 };
 
+// BwdEpiL with the activation factor from the forward's sign-bit mask (FwdEpiM) staged in
+// LDS: 1 + bit, the value the z-based epilogue computes (same comparison, made once in the
+// forward), so G is bitwise the same.  Used for the hidden layers (l >= 1) only.
+template <typename T>
+struct BwdEpiLM {
+  struct Col {
+    T f[4];
+  };
+  const uint8_t* m;  // LDS mask tile (FwdEpiM's layout) at this layer's offset
+  int rows_live, lane;
+  T* out;
+  __device__ __forceinline__ Col load(int col, bool valid) const {
+    Col k;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = Mfma<T>::row(lane, i);
+      const uint32_t h = m[(col >> 4) * 64 + 16 * (row >> 2) + (col & 15)];
+      k.f[i] = (valid && row < rows_live && ((h >> (row & 3)) & 1u)) ? T(2) : T(1);
+    }
+    return k;
+  }
+  __device__ __forceinline__ void store(int i, int row, int col, bool valid, T acc, const Col& k) const {
+    out[row * kNnLd + col] = valid ? acc * k.f[i] : T(0);
+  }
+};
+
 // The writer wave: G block `width` wide of the workgroup's rows from the LDS image `img`
 // (row stride kNnLd) to G rows (stride gtot) at column offset goff.  Lane l owns vector
 // q = l % per_row of rows l / per_row + k * (64 / per_row); four passes' LDS reads are in
@@ -208,7 +241,7 @@ __device__ __forceinline__ void write_G_block(const T* img, int width, T* G, int
       write_G_rows<T, 1>(img + c0, width - c0 < 64 ? width - c0 : 64, G, gtot, goff + c0, rows_live, lane);
 }
 
-template <typename T, class E, int D, int SCHEME, bool ZST, bool FAST>
+template <typename T, class E, int D, int SCHEME, bool ZST, bool FAST, bool MASK = false>
 __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, const DevConsts<T> c,
                                                                   const NnMlp<T> mlp,
                                                                   const NnBackArgs<T> a) {
@@ -231,7 +264,8 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
   const int L = mlp.L;
   int wsum = 0;
   for (int i = 0; i <= L + 1; ++i) wsum += mlp.width[i];
-  const PL pl(wsum, mlp.ztot, ZST);
+  static_assert(!MASK || (FAST && !ZST), "the mask replaces z staging on the fast path");
+  const PL pl(wsum, mlp.ztot, ZST, MASK ? a.mb : 0);
   T* s_bn = reinterpret_cast<T*>(s_dyn + pl.bn);  // [scale image | shift image], column goff[i]
   auto s_in = [&](int par) { return s_dyn + pl.in + (uint32_t)par * PL::kPar; };
   auto s_z = [&](int par) { return reinterpret_cast<const T*>(s_dyn + pl.z + (uint32_t)par * pl.zpar); };
@@ -249,6 +283,11 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
     wave_copy_lds<4>(a.flag + rt, (uint32_t)(rows_live * 4), b + PL::kFlag, lane);
   };
   auto stage_z = [&](int ts, int par, uint32_t part) {
+    if constexpr (MASK) {  // the sign-bit tile (mb bytes, padded rows included): one share
+      if (part == 0)
+        wave_copy_lds<16>(a.mask + ((int64_t)ts * ((a.B + 15) >> 4) + (row0 >> 4)) * a.mb,
+                          (uint32_t)a.mb, s_dyn + pl.z + (uint32_t)par * pl.zpar, lane);
+    }
     if constexpr (ZST) {
       const int64_t rt = (int64_t)ts * a.B + row0;
 #if DPAC_BWD2_ZREG
@@ -376,7 +415,21 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
         BwdEpiL<T> epi{l >= 1 ? s_bn + a.goff[l] : nullptr, l >= 1 ? s_bn + wsum + a.goff[l] : nullptr,
                        ZST ? s_z(par) + mlp.zoff[l] : a.z + (rowt + row0) * mlp.ztot + mlp.zoff[l],
                        mlp.ztot, rows_live, lane, out};
-        if constexpr (FAST) {
+        if constexpr (MASK) {
+          if (l >= 1) {  // hidden layer l: its mask rows sit at halfword 13 (l - 1)
+            BwdEpiLM<T> epm{reinterpret_cast<const uint8_t*>(s_dyn + pl.z + (uint32_t)par * pl.zpar) + 13 * 64 * (l - 1),
+                            rows_live, lane, out};
+            if (l == L) {
+              if (L >= 2) load_wide_pre(pre, a.wtkm[L - 1], mlp.width[L], mlp.width[L - 1], wave, lane);
+              nn_layer_narrow_in(in, K, Nout, res_in, wave, lane, epm);
+            } else {
+              nn_layer_wide(in, Nout, a.wtkm[l], pre, wave, lane, epm);
+              if (l >= 2) load_wide_pre(pre, a.wtkm[l - 1], mlp.width[l], mlp.width[l - 1], wave, lane);
+            }
+          } else {
+            nn_layer_narrow_out(in, K, Nout, res_out, wave, lane, epi);
+          }
+        } else if constexpr (FAST) {
           if (l == L) {
             if (L >= 2) load_wide_pre(pre, a.wtkm[L - 1], mlp.width[L], mlp.width[L - 1], wave, lane);
             nn_layer_narrow_in(in, K, Nout, res_in, wave, lane, epi);

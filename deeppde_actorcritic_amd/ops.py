@@ -197,7 +197,10 @@ def rollout_nn(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor, total_time:
     solver.py:260-278), one launch of dpac_rollout_nn_fwd.
 
     Returns (x [N+1,B,d], dt [B,N], coef [B,N], u [N,B,c] | None, y | None, disc | None,
-    saves | None) with saves = (z [N,B,Σ widths[1:]], flag [N,B] int32, disc_t [N,B])."""
+    saves | None) with saves = (z [N,B,Σ widths[1:]], flag [N,B] int32, disc_t [N,B], mask)
+    and mask the hidden activations' sign bits [N,ceil(B/16),mask_tile_bytes] (uint8, dpac.h)
+    where the kernel wrote them
+    (the float 16-row fast path: dpac_rollout_nn_fwd_masked), else None."""
     _require_gpu(x0, dw, *mlp.tensors)
     _check_same(x0, dw, *mlp.tensors)
     B, d = x0.shape
@@ -213,15 +216,21 @@ def rollout_nn(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor, total_time:
     if cost_order is not None:
         y = torch.empty(B, **kw)
         disc = torch.empty(B, **kw)
-    saves = None
+    saves = mask = None
+    written = ctypes.c_int32(0)
     if save:
         saves = (torch.empty(N, B, sum(mlp.widths[1:]), **kw),
                  torch.empty(N, B, dtype=torch.int32, device=x0.device), torch.empty(N, B, **kw))
-    call("dpac_rollout_nn_fwd", ctypes.byref(eqp), scheme, _dtype_id(x0), B, N, float(total_time),
+        mb = _lib.load().dpac_rollout_nn_mask_tile_bytes(ctypes.byref(mlp.struct))
+        if MASK_BPTT and x0.dtype == torch.float32 and mb > 0:
+            mask = torch.empty(N, (B + 15) // 16, mb, dtype=torch.uint8, device=x0.device)
+    call("dpac_rollout_nn_fwd_masked", ctypes.byref(eqp), scheme, _dtype_id(x0), B, N, float(total_time),
          ctypes.byref(mlp.struct), _ptr(x0.contiguous()), _ptr(dw.contiguous()), _ptr(x), _ptr(dt),
          _ptr(coef), _ptr(u), _lib.COST_CRITIC if cost_order is None else cost_order, _ptr(y),
          _ptr(disc), _ptr(saves[0] if saves else None), _ptr(saves[1] if saves else None),
-         _ptr(saves[2] if saves else None), _stream(x0))
+         _ptr(saves[2] if saves else None), _ptr(mask), ctypes.byref(written), _stream(x0))
+    if saves is not None:
+        saves = saves + (mask if written.value else None,)
     return x, dt, coef, u, y, disc, saves
 
 
@@ -243,9 +252,10 @@ class _ActorRolloutNN(torch.autograd.Function):
         L = (len(params) - 1) // 3 - 1
         gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
         view, _, _ = mlp_prepare(gam, bet, Ws, b, ekn, False)
-        x, dt, coef, u, y, disc, (z, flag, disc_t) = rollout_nn(
+        x, dt, coef, u, y, disc, (z, flag, disc_t, mask) = rollout_nn(
             eqp, scheme, x0, dw, T, N, view, cost_order=_lib.COST_ACTOR, save=True)
         ctx.save_for_backward(x, u, dw, z, flag, disc_t, rs, *params)
+        ctx.mask = mask  # None where the forward kernel wrote no mask
         ctx.cfg = (eqp, scheme, T, N, ekn, L)
         return y, disc, x[N].clone()
 
@@ -253,26 +263,27 @@ class _ActorRolloutNN(torch.autograd.Function):
     def backward(ctx, g_y, g_disc, g_xN):
         x, u, dw, z, flag, disc_t, rs, *params = ctx.saved_tensors
         eqp, scheme, T, N, ekn, L = ctx.cfg
-        grads = actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, (x, u, dw, z, flag, disc_t),
+        grads = actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, (x, u, dw, z, flag, disc_t, ctx.mask),
                                  g_y, g_disc, g_xN)
         return (None,) * 8 + tuple(grads)
 
 
 def actor_rollout_saves(eqp, scheme: int, x0, dw, total_time: float, num_steps: int, net):
     """The actor's rollout with `net` as control and the backward saves, no autograd:
-    (y [B], disc_N [B], x_N [B, d], saved) with saved = (x, u, dw, z, flag, disc_t) as
+    (y [B], disc_N [B], x_N [B, d], saved) with saved = (x, u, dw, z, flag, disc_t, mask) as
     actor_bptt_grads takes it (the forward of _ActorRolloutNN)."""
-    x, dt, coef, u, y, disc, (z, flag, disc_t) = rollout_nn(
+    x, dt, coef, u, y, disc, (z, flag, disc_t, mask) = rollout_nn(
         eqp, scheme, x0, dw, total_time, num_steps, net.mlp_view(), cost_order=_lib.COST_ACTOR,
         save=True)
-    return y, disc, x[num_steps], (x, u, dw.contiguous(), z, flag, disc_t)
+    return y, disc, x[num_steps], (x, u, dw.contiguous(), z, flag, disc_t, mask)
 
 
 def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_xN):
     """Gradients of DeepNN.trainable_variables() (params) of the actor from the saves of
     its fused rollout and the upstream gradients of (y, disc_N, x_N), each optional:
     the BPTT of solver.py:92-97 (dpac_rollout_nn_bwd, then dpac_mlp_param_grads)."""
-    x, u, dw, z, flag, disc_t = saved
+    x, u, dw, z, flag, disc_t = saved[:6]
+    mask = saved[6] if len(saved) > 6 else None
     L = (len(params) - 1) // 3 - 1
     gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
     B, d = x.shape[1], x.shape[2]
@@ -286,7 +297,7 @@ def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_x
     gy_in = None if g_y is None else g_y.contiguous()
     if BPTT_MODE == "fused":
         G = _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km, widths,
-                        gx_in, gd_in, gy_in)
+                        gx_in, gd_in, gy_in, mask)
     else:
         G = _bptt_loop(eqp, scheme, T, N, ekn, L, x, u, dw, zl, flag, disc_t, s, bet, Ws, b,
                        widths, gx_in, gd_in, gy_in)
@@ -309,6 +320,9 @@ def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_x
     return [*dgam, *dbet, *dW, db]
 
 
+# The actor's forward records the hidden activations' sign bits and the BPTT reads them
+# instead of z (dpac_rollout_nn_*_masked; bitwise the same G).  False: z everywhere.
+MASK_BPTT = os.environ.get("DPAC_MASK_BPTT", "1") != "0"
 # "fused": the reverse time loop as one dpac_rollout_nn_bwd launch; "loop": the
 # reference implementation of the same loop, dpac_step_bwd + PyTorch per step.
 BPTT_MODE = "fused"
@@ -381,16 +395,16 @@ def _ptr_array(ts):
 
 
 def _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km, widths,
-                g_xN, g_disc, g_y):
+                g_xN, g_disc, g_y, mask=None):
     """G[i] = dL/d(output of BN_i) for every step, [N, B, width[i]], from one launch
-    (view, wt, wt_km from mlp_prepare)."""
+    (view, wt, wt_km from mlp_prepare; mask: the forward's sign bits, or None)."""
     B = x.shape[1]
     goff = np.cumsum([0] + widths).tolist()
     Gall = torch.empty(N, B, goff[-1], dtype=x.dtype, device=x.device)
-    call("dpac_rollout_nn_bwd", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
+    call("dpac_rollout_nn_bwd_masked", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
          ctypes.byref(view.struct), _ptr_array(wt), _ptr_array(wt_km), _ptr(x), _ptr(u), _ptr(dw),
-         _ptr(z), _ptr(flag), _ptr(disc_t), _ptr(g_xN), _ptr(g_disc), _ptr(g_y), _ptr(Gall), None,
-         _stream(x))
+         _ptr(z), _ptr(flag), _ptr(disc_t), _ptr(mask), _ptr(g_xN), _ptr(g_disc), _ptr(g_y), _ptr(Gall),
+         None, _stream(x))
     return [Gall[:, :, goff[i]:goff[i + 1]] for i in range(L + 2)]
 
 

@@ -282,6 +282,34 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
                         const int32_t* save_flag, const void* save_disc, const void* g_xN,
                         const void* g_disc, const void* g_y, void* G, void* g_x0, void* stream);
 
+/* The same forward / BPTT pair with a sign-bit mask: the BPTT needs of the saved pre-BN
+ * outputs z only whether each hidden BN output was positive (the activation factor
+ * 1 + [y > 0]); dpac_rollout_nn_fwd_masked records those bits as the forward computes
+ * them, save_mask [N][ceil(B / 16)][dpac_rollout_nn_mask_tile_bytes(actor)] bytes (per
+ * 16-row tile: row r of hidden layer l, column c at bit r % 4 of byte
+ * 13*64 l + 64 (c / 16) + 16 (r / 4) + c % 16, the MFMA accumulator's lane layout), and
+ * dpac_rollout_nn_bwd_masked reads them instead of z (z is still needed by the parameter
+ * gradients and the Eikonal head).  The mask is written only on the float 16-row fast path
+ * (hidden layers 193..208 wide, d and out <= 32, k-major images, batches > 1024 or
+ * DPAC_NN_TILE=16): *mask_written (host) reports whether it was; pass it to the backward only
+ * then.  Results are bitwise those of the unmasked pair. */
+int32_t dpac_rollout_nn_mask_tile_bytes(const dpac_mlp* actor);
+int dpac_rollout_nn_fwd_masked(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                               int64_t num_sample, int32_t num_steps, double total_time,
+                               const dpac_mlp* actor, const void* x0, const void* dw, void* x,
+                               void* dt, void* coef, void* u, int32_t cost_order, void* y,
+                               void* disc, void* save_z, int32_t* save_flag, void* save_disc,
+                               uint8_t* save_mask, int32_t* mask_written, void* stream);
+int dpac_rollout_nn_bwd_masked(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
+                               int64_t num_sample, int32_t num_steps, double total_time,
+                               const dpac_mlp* actor, const void* const* weight_t,
+                               const void* const* weight_t_km, const void* x,
+                               const void* u, const void* dw, const void* save_z,
+                               const int32_t* save_flag, const void* save_disc,
+                               const uint8_t* save_mask, const void* g_xN,
+                               const void* g_disc, const void* g_y, void* G, void* g_x0,
+                               void* stream);
+
 /* ---- a dpac_mlp over independent rows (the critic's networks) -------------
  * Forward: out [rows][width[n_hidden+1]] = the network (bn_0 -> (dense -> bn ->
  * y+relu(y)) x n_hidden -> dense(+bias) -> bn_last, solver.py:260-271) applied to

@@ -115,8 +115,9 @@ def test_backward_saves_and_cost():
     net, _ = actor_pair(cfg, torch.float64)
     eqp = ep.params()
     x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=6, dtype=torch.float64, device=DEV)
-    x, dt, coef, u, y, disc, (z, flag, disc_t) = ops.rollout_nn(
+    x, dt, coef, u, y, disc, (z, flag, disc_t, mask) = ops.rollout_nn(
         eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, net.mlp_view(), cost_order=_lib.COST_ACTOR, save=True)
+    assert mask is None  # sign-bit masks are a float 16-row fast-path product
     # pre-BN layer outputs, recomputed with PyTorch from the recorded states
     rs, g, bt, W = net.bn_rs, net.bn_gamma, net.bn_beta, net.W
     with torch.no_grad():
@@ -326,7 +327,7 @@ def test_bptt_stager_writer_kernel_bitwise(name, d, hidden, B, dtype, scheme):
     sch = SCHEMES[scheme]
     x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=8, dtype=dtype, device=DEV)
     y, disc, xN, saved = ops.actor_rollout_saves(eqp, sch, x0, dw, T, N, net)
-    x, u, dwc, z, flag, disc_t = saved
+    x, u, dwc, z, flag, disc_t, _ = saved
     params = [p.detach() for p in net.trainable_variables()]
     L = len(hidden)
     gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
@@ -385,7 +386,7 @@ def test_actor_fast_path_bitwise(name, d, hidden, B, scheme):
         os.environ["DPAC_NN_TILE"] = "16"
         for f in ("0", "1"):
             os.environ["DPAC_NN_FAST"] = f
-            fwd[f] = [t.clone() if torch.is_tensor(t) else [s.clone() for s in t]
+            fwd[f] = [t.clone() if torch.is_tensor(t) else [s.clone() for s in t[:3]]
                       for t in ops.rollout_nn(eqp, sch, x0, dw, T, N, view, cost_order=_lib.COST_ACTOR, save=True)]
             x, _, _, u, _, _, (z, flag, disc_t) = fwd[f]
             G = ops._bptt_fused(eqp, sch, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km, widths,
@@ -402,3 +403,66 @@ def test_actor_fast_path_bitwise(name, d, hidden, B, scheme):
             assert torch.equal(s, t)
     assert torch.isfinite(bwd["1"]).all()
     assert torch.equal(bwd["0"], bwd["1"])
+
+
+@pytest.mark.parametrize("name,d,hidden,B,scheme", [
+    ("LQR", 20, (200, 200, 200), 2048, "adaptive"),
+    ("EKN", 20, (200, 200, 200), 37, "naive"),
+    ("VDP", 20, (200, 200), 50, "adaptive"),
+    ("LQR", 4, (208, 200, 193), 20, "adaptive"),
+    ("LQR_var", 20, (200,), 17, "naive")])
+def test_bptt_sign_mask_bitwise(name, d, hidden, B, scheme, monkeypatch):
+    """The actor forward's sign-bit mask (dpac_rollout_nn_fwd_masked: bit r % 4 of byte
+    [13 l + c/16][r/4 % 4][c % 16] of row r's 16-row tile = [BN_{l+1}(z) > 0] of hidden layer
+    l) leaves every forward output
+    bitwise unchanged, matches the signs recomputed from the saved z, and the BPTT reading
+    it (dpac_rollout_nn_bwd_masked) gives bitwise the G of the z-based BPTT."""
+    N, T = 12, 0.2
+    cfg = full_config(name, d, N=N, hidden=hidden, scheme=scheme, dtype="float32")
+    ep = getattr(peq, name)(cfg.eqn_config)
+    net, _ = actor_pair(cfg, torch.float32)
+    eqp = ep.params()
+    sch = SCHEMES[scheme]
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=13, dtype=torch.float32, device=DEV)
+    params = [p.detach() for p in net.trainable_variables()]
+    L = len(hidden)
+    gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
+    widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+    view, wt, wt_km = ops.mlp_prepare(gam, bet, Ws, b, net.ekn_head, True)
+    monkeypatch.setenv("DPAC_NN_TILE", "16")
+    monkeypatch.setenv("DPAC_NN_FAST", "1")
+    fwd = {}
+    for m in (False, True):
+        monkeypatch.setattr(ops, "MASK_BPTT", m)
+        fwd[m] = ops.rollout_nn(eqp, sch, x0, dw, T, N, view, cost_order=_lib.COST_ACTOR, save=True)
+    assert fwd[False][6][3] is None
+    mask = fwd[True][6][3]
+    mb = _lib.load().dpac_rollout_nn_mask_tile_bytes(ctypes.byref(view.struct))
+    assert mb == 13 * 64 * L and mask is not None and mask.shape == (N, (B + 15) // 16, mb)
+    for a, c in zip(fwd[False][:6], fwd[True][:6]):
+        assert (a is None and c is None) or torch.equal(a, c)
+    for a, c in zip(fwd[False][6][:3], fwd[True][6][:3]):
+        assert torch.equal(a, c)
+    # the bits against the signs of BN(z) recomputed here (borderline |y| excluded)
+    x, _, _, u, _, _, (z, flag, disc_t, _) = fwd[True]
+    # [N, tiles, 13 L col tiles, 4 row quads, 16 cols] -> bit r % 4 -> [N, rows, 13 L * 16 cols]
+    m5 = mask.to(torch.int32).reshape(N, -1, 13 * L, 4, 16)
+    bits = torch.stack([(m5 >> k) & 1 for k in range(4)], 4)  # [N, tiles, ct, quad, row%4, 16]
+    bits = bits.permute(0, 1, 3, 4, 2, 5).reshape(N, -1, 13 * L * 16)[:, :B]
+    off = 0
+    for l in range(L):
+        w = widths[l + 1]
+        zl = z[:, :, off:off + w]
+        off += w
+        yl = bet[l + 1] + zl * (net.bn_rs * gam[l + 1])
+        got = bits[:, :, 13 * 16 * l:13 * 16 * l + w]
+        clear = yl.abs() > 1e-5 * (1 + yl.abs().max())
+        assert torch.equal(got[clear].bool(), (yl > 0)[clear])
+    g_y = torch.full((B,), 1.0 / B, device=DEV)
+    G = {}
+    for use in (None, mask):
+        G[use is None] = ops.G_all(ops._bptt_fused(
+            eqp, sch, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km, widths,
+            torch.ones_like(x[-1]) * 0.01, torch.full_like(g_y, 0.5), g_y, use)).clone()
+    assert torch.isfinite(G[False]).all()
+    assert torch.equal(G[True], G[False])

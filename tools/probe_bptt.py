@@ -58,7 +58,7 @@ def main():
         sch = _lib.SCHEME_ADAPTIVE
         fwd = lambda: ops.actor_rollout_saves(eqp, sch, x0, dw, 0.2, N, net)
         y, disc, xN, saved = fwd()
-        x, u, dwc, z, flag, disc_t = saved
+        x, u, dwc, z, flag, disc_t, mask = saved
         params = net.trainable_variables()
         L = 3
         gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
@@ -69,7 +69,7 @@ def main():
         g_disc = torch.rand_like(y) / B
         g_xN = torch.randn_like(xN) / B
         bwd = lambda: ops._bptt_fused(eqp, sch, 0.2, N, L, x, u, dwc, z, flag, disc_t, view, wt, wt_km, widths,
-                                      g_xN, g_disc, g_y)
+                                      g_xN, g_disc, g_y, mask)
         G = bwd()
         Gall = ops.G_all(G)
         pg = lambda: ops.mlp_param_grads(view, x[:N].reshape(N * B, 20), z.reshape(N * B, -1),

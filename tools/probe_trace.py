@@ -65,7 +65,7 @@ def main():
     torch.cuda.synchronize()
     steps = np.arange(8, 62)
     res = {"B": B, "N": N, "fwd": table(lib, 8, FWD_POINTS, steps)}
-    x, u, dwc, z, flag, disc_t = saved
+    x, u, dwc, z, flag, disc_t, mask = saved
     params = net.trainable_variables()
     L = 3
     gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
@@ -74,7 +74,7 @@ def main():
                                       [p.detach() for p in Ws], b.detach(), False, True)
     g_y = torch.full_like(y, 1.0 / B)
     ops._bptt_fused(eqp, sch, 0.2, N, L, x, u, dwc, z, flag, disc_t, view, wt, wt_km, widths,
-                    torch.randn_like(xN) / B, torch.rand_like(y) / B, g_y)
+                    torch.randn_like(xN) / B, torch.rand_like(y) / B, g_y, mask)
     torch.cuda.synchronize()
     # the BPTT walks t = N-1 .. 0: steps 8..61 are its last ones
     res["bwd"] = table(lib, 10, BWD_POINTS, steps, rev=True)

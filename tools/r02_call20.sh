@@ -1,5 +1,5 @@
-# Round-2 call 18: the BPTT sign-bit mask: NN tests (bitwise masked vs z-based), BPTT
-# timing with the mask on/off, and the training iteration on/off.
+# Round-2 call 20: the per-lane nibble sign-bit mask (accumulator layout): NN tests, BPTT
+# timing with the mask on/off, and the training iteration.
 source tools/gpu_steps.sh
 export TMPDIR=/tmp
 rm -f gpurun_out/steps.log
@@ -8,5 +8,3 @@ run 120 bptt_mask python -u tools/probe_bptt.py --B 2048,4096 --N 100 --reps 10
 DPAC_MASK_BPTT=0 run 120 bptt_nomask python -u tools/probe_bptt.py --B 2048,4096 --N 100 --reps 10
 run 200 train_mask python -u tools/train_bench.py --iters 20 --batch 2048
 DPAC_MASK_BPTT=0 run 200 train_nomask python -u tools/train_bench.py --iters 20 --batch 2048
-run 200 train_mask4k python -u tools/train_bench.py --iters 20 --batch 4096
-run 400 models python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_models.py
