@@ -574,10 +574,19 @@ __device__ __forceinline__ void mfma_rows16_res(const float* in, int Nout, const
   }
 }
 
-// mfma_rows16_kms<NT, NG> with its first PG groups of B already in registers
-template <int NT, int NG, class EPI>
+#ifndef DPAC_NN_PRE_EARLY
+#define DPAC_NN_PRE_EARLY 1  // 0: the next layer's prefetch after the epilogue (timing knob)
+#endif
+struct NoNext {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// mfma_rows16_kms<NT, NG> with its first PG groups of B already in registers; nx() runs
+// between the products and the epilogue (the next layer's weight prefetch: issued there,
+// its loads are not queued behind this epilogue's z / mask stores in vmcnt order)
+template <int NT, int NG, class EPI, class NX = NoNext>
 __device__ __forceinline__ void mfma_rows16_kms_pre(const float* in, int Nout, const float* Wkm, const WidePre& pre,
-                                                    int wave, int lane, EPI& epi) {
+                                                    int wave, int lane, EPI& epi, NX nx = NX{}) {
   using MF = Mfma<float>;
   constexpr int K16 = 16 * NG;
   constexpr int PG = DPAC_NN_KMS_PG < NG ? DPAC_NN_KMS_PG : NG;
@@ -618,12 +627,18 @@ __device__ __forceinline__ void mfma_rows16_kms_pre(const float* in, int Nout, c
     // (one load in flight, the L2 latency exposed every 4 MFMAs)
     __builtin_amdgcn_sched_barrier(0);
   }
+#if DPAC_NN_PRE_EARLY
+  nx();
+#endif
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = (wave + kNnWaves * j) * 16 + col_l;
 #pragma unroll
     for (int i = 0; i < 4; ++i) epi.store(i, MF::row(lane, i), col, col < Nout, acc[j][i], cc[j]);
   }
+#if !DPAC_NN_PRE_EARLY
+  nx();
+#endif
 }
 
 // mfma_rows16_splitk's k-major branch with the wave's slice of B in registers
@@ -695,12 +710,12 @@ __device__ __forceinline__ void nn_layer_narrow_in(const float* in, int K, int N
   }
 }
 
-template <class EPI>
+template <class EPI, class NX = NoNext>
 __device__ __forceinline__ void nn_layer_wide(const float* in, int Nout, const float* Wkm, const WidePre& pre,
-                                              int wave, int lane, EPI& epi) {
+                                              int wave, int lane, EPI& epi, NX nx = NX{}) {
   const int mine = nn_mine(Nout, wave);
-  if (mine == 1) mfma_rows16_kms_pre<1, 13>(in, Nout, Wkm, pre, wave, lane, epi);
-  else if (mine == 2) mfma_rows16_kms_pre<2, 13>(in, Nout, Wkm, pre, wave, lane, epi);
+  if (mine == 1) mfma_rows16_kms_pre<1, 13>(in, Nout, Wkm, pre, wave, lane, epi, nx);
+  else if (mine == 2) mfma_rows16_kms_pre<2, 13>(in, Nout, Wkm, pre, wave, lane, epi, nx);
 }
 
 template <class EPI>
@@ -1063,8 +1078,9 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
             if (L >= 2) load_wide_pre(pre, mlp.wkm[1], mlp.width[1], mlp.width[2], wave, lane);
             nn_layer_narrow_in(in, mlp.width[0], mlp.width[1], res_in, wave, lane, epm);
           } else {
-            nn_layer_wide(in, mlp.width[l + 1], mlp.wkm[l], pre, wave, lane, epm);
-            if (l + 1 < L) load_wide_pre(pre, mlp.wkm[l + 1], mlp.width[l + 1], mlp.width[l + 2], wave, lane);
+            nn_layer_wide(in, mlp.width[l + 1], mlp.wkm[l], pre, wave, lane, epm, [&]() {
+              if (l + 1 < L) load_wide_pre(pre, mlp.wkm[l + 1], mlp.width[l + 1], mlp.width[l + 2], wave, lane);
+            });
           }
         } else if (l == 0) {
           if (L >= 2) load_wide_pre(pre, mlp.wkm[1], mlp.width[1], mlp.width[2], wave, lane);
@@ -1073,8 +1089,9 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
         } else if (l == L) {
           nn_layer_narrow_out(in, mlp.width[L], mlp.width[L + 1], res_out, wave, lane, epi);
         } else {
-          nn_layer_wide(in, mlp.width[l + 1], mlp.wkm[l], pre, wave, lane, epi);
-          if (l + 1 < L) load_wide_pre(pre, mlp.wkm[l + 1], mlp.width[l + 1], mlp.width[l + 2], wave, lane);
+          nn_layer_wide(in, mlp.width[l + 1], mlp.wkm[l], pre, wave, lane, epi, [&]() {
+            if (l + 1 < L) load_wide_pre(pre, mlp.wkm[l + 1], mlp.width[l + 1], mlp.width[l + 2], wave, lane);
+          });
         }
       } else {
         mfma_layer<T>(in, mlp.width[l], mlp.width[l + 1], mlp.weight[l], mlp.wkm[l], wave, lane, epi);

@@ -423,8 +423,9 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
               if (L >= 2) load_wide_pre(pre, a.wtkm[L - 1], mlp.width[L], mlp.width[L - 1], wave, lane);
               nn_layer_narrow_in(in, K, Nout, res_in, wave, lane, epm);
             } else {
-              nn_layer_wide(in, Nout, a.wtkm[l], pre, wave, lane, epm);
-              if (l >= 2) load_wide_pre(pre, a.wtkm[l - 1], mlp.width[l], mlp.width[l - 1], wave, lane);
+              nn_layer_wide(in, Nout, a.wtkm[l], pre, wave, lane, epm, [&]() {
+                if (l >= 2) load_wide_pre(pre, a.wtkm[l - 1], mlp.width[l], mlp.width[l - 1], wave, lane);
+              });
             }
           } else {
             nn_layer_narrow_out(in, K, Nout, res_out, wave, lane, epi);
@@ -436,8 +437,9 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
           } else if (l == 0) {
             nn_layer_narrow_out(in, K, Nout, res_out, wave, lane, epi);
           } else {
-            nn_layer_wide(in, Nout, a.wtkm[l], pre, wave, lane, epi);
-            if (l >= 2) load_wide_pre(pre, a.wtkm[l - 1], mlp.width[l], mlp.width[l - 1], wave, lane);
+            nn_layer_wide(in, Nout, a.wtkm[l], pre, wave, lane, epi, [&]() {
+              if (l >= 2) load_wide_pre(pre, a.wtkm[l - 1], mlp.width[l], mlp.width[l - 1], wave, lane);
+            });
           }
         } else {
           mfma_layer<T>(in, K, Nout, a.wt[l], a.wtkm[l], wave, lane, epi);
