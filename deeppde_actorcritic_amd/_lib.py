@@ -18,7 +18,7 @@ DPAC_OK, DPAC_EINVAL, DPAC_EUNSUP = 0, -1, -2
 F32, F64 = 0, 1
 EQN_LQR, EQN_VDP, EQN_EKN, EQN_LQR_VAR = 0, 1, 2, 3
 SCHEME_NAIVE, SCHEME_ADAPTIVE = 0, 1
-TD1, TD2 = 1, 2
+TD1, TD2, TD1_GDOT = 1, 2, 3
 COST_CRITIC, COST_ACTOR = 0, 1
 SAMPLE_NORMAL, SAMPLE_BOUNDED, SAMPLE_ZERO_X0 = 0, 1, 2
 (EVAL_DRIFT, EVAL_SIGMA, EVAL_W, EVAL_Z, EVAL_V_TRUE, EVAL_U_TRUE, EVAL_V_GRAD,
@@ -86,6 +86,7 @@ SIGNATURES = {
                              _P, _P, _P, _P, _P],
     "dpac_td_assemble_bwd": [_EQ, _I32, _I64, _I32, _P, _P, _P, _U64, _I64, _I32, _P, _P, _P, _P,
                              _P],
+    "dpac_td_assemble_bwd_gdot": [_EQ, _I32, _I64, _I32, _P, _P, _P, _P, _P],
     "dpac_actor_cost_fwd": [_EQ, _I32, _I64, _I32, _P, _P, _P, _P, _P, _P, _P],
     "dpac_equation_eval": [_EQ, _I32, _I32, _I64, _P, _P, _P, _P],
     "dpac_rollout_nn_fwd": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp), _P, _P, _P, _P,
@@ -102,6 +103,9 @@ SIGNATURES = {
     "dpac_mlp_rows_fwd": [_I32, _I64, ctypes.POINTER(Mlp), _P, _I64, _P, _P, _P],
     "dpac_mlp_rows_bwd": [_I32, _I64, ctypes.POINTER(Mlp), ctypes.POINTER(ctypes.c_void_p),
                           ctypes.POINTER(ctypes.c_void_p), _P, _P, _P, _P, _P],
+    "dpac_mlp_rows_fwd_td1": [_EQ, _I32, _I64, ctypes.POINTER(Mlp), _P, _I64, _P, _P, _P, _P, _P],
+    "dpac_mlp_rows_bwd_td1": [_EQ, _I32, _I64, ctypes.POINTER(Mlp), ctypes.POINTER(ctypes.c_void_p),
+                              ctypes.POINTER(ctypes.c_void_p), _P, _P, _I64, _P, _P, _P, _P, _P, _P],
     "dpac_mlp_param_grads_workspace": [_I32, _I64, ctypes.POINTER(Mlp)],
     "dpac_mlp_param_grads": [_I32, _I64, ctypes.POINTER(Mlp), _D, _P, _I64, _P, _P, _P, _I64, _P,
                              _P],

@@ -25,9 +25,10 @@ int mlp_param_grads_launch(int dtype, int64_t rows, const dpac_mlp& net, double 
                            const void* x, int64_t ldx, const void* z, const void* G, void* ws,
                            void* out, hipStream_t s);
 int mlp_rows_fwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx,
-                        void* out, void* save_z, hipStream_t s);
+                        void* out, void* save_z, const TdRows* td, hipStream_t s);
 int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
-                        const void* save_z, const void* g_out, void* G, void* g_x, hipStream_t s);
+                        const void* save_z, const void* g_out, void* G, void* g_x, const TdRows* td,
+                        hipStream_t s);
 int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
                        void* wkm, void* wtkm, hipStream_t s);
 int adam_launch(int dtype, int n, const int64_t* numel, void* const* var, const void* const* grad,
@@ -473,7 +474,7 @@ int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
     if (!net->weight[i]) return fail(DPAC_EINVAL, "weight[%d] is NULL", i);
   DPAC_REQUIRE(x);
   DPAC_REQUIRE(out);
-  const int r = mlp_rows_fwd_launch(dtype, rows, *net, x, ldx, out, save_z, (hipStream_t)stream);
+  const int r = mlp_rows_fwd_launch(dtype, rows, *net, x, ldx, out, save_z, nullptr, (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();
 }
@@ -492,7 +493,69 @@ int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
     if (!weight_t[i]) return fail(DPAC_EINVAL, "weight_t[%d] is NULL", i);
   dpac_mlp bnet = *net;  // the struct's weight_km (forward images) never reach the backward
   for (int i = 0; i <= net->n_hidden; ++i) bnet.weight_km[i] = weight_t_km ? weight_t_km[i] : nullptr;
-  const int r = mlp_rows_bwd_launch(dtype, rows, bnet, weight_t, save_z, g_out, G, g_x,
+  const int r = mlp_rows_bwd_launch(dtype, rows, bnet, weight_t, save_z, g_out, G, g_x, nullptr,
+                                    (hipStream_t)stream);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
+}
+
+// The equation's elementwise sigma as (sa, sb) and k_td's lane split, for the fused
+// TD1 entry points (dpac_mlp_rows.h: TdRows).
+static int td_rows_setup(const dpac_eqn_params* eq, int32_t dtype, int64_t rows, const dpac_mlp* net,
+                         dpac::TdRows& td) {
+  if (int e = check_common(eq, dtype, rows)) return e;
+  if (int e = check_net(net)) return e;
+  const int d = eq->dim;
+  if (net->width[net->n_hidden + 1] != d)
+    return fail(DPAC_EINVAL, "the network's output width (%d) must equal dim (%d)",
+                net->width[net->n_hidden + 1], d);
+  if (net->width[0] != d)
+    return fail(DPAC_EINVAL, "the network's input width (%d) must equal dim (%d)", net->width[0], d);
+  td.p = eq->eqn == DPAC_EQN_VDP ? 1 : lanes_for_dim(d);  // E::kP of the equation's k_td
+  td.sa = 1.4142135623730951;                               // np.sqrt(2.0) (equation.py:170)
+  td.sb = eq->eqn == DPAC_EQN_LQR_VAR ? eq->epsilon : 0.0;  // LQR_var: sqrt2*(1 + eps*x*u) (:302)
+  td.ldu = eq->control_dim;
+  return 0;
+}
+
+int dpac_mlp_rows_fwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows, const dpac_mlp* net,
+                          const void* x, int64_t ldx, const void* u, const void* dw, void* gdot,
+                          void* save_z, void* stream) {
+  dpac::TdRows td{};
+  if (int e = td_rows_setup(eq, dtype, rows, net, td)) return e;
+  if (ldx < eq->dim) return fail(DPAC_EINVAL, "ldx (%lld) < dim (%d)", (long long)ldx, eq->dim);
+  for (int i = 0; i <= net->n_hidden; ++i)
+    if (!net->weight[i]) return fail(DPAC_EINVAL, "weight[%d] is NULL", i);
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(dw);
+  DPAC_REQUIRE(gdot);
+  if (td.sb != 0.0) DPAC_REQUIRE(u);
+  td.x = x; td.ldx = ldx; td.u = u; td.dw = dw; td.gdot = gdot;
+  const int r = mlp_rows_fwd_launch(dtype, rows, *net, x, ldx, nullptr, save_z, &td, (hipStream_t)stream);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
+}
+
+int dpac_mlp_rows_bwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows, const dpac_mlp* net,
+                          const void* const* weight_t, const void* const* weight_t_km,
+                          const void* save_z, const void* x, int64_t ldx, const void* u,
+                          const void* dw, const void* g_gdot, void* G, void* g_x, void* stream) {
+  dpac::TdRows td{};
+  if (int e = td_rows_setup(eq, dtype, rows, net, td)) return e;
+  if (ldx < eq->dim) return fail(DPAC_EINVAL, "ldx (%lld) < dim (%d)", (long long)ldx, eq->dim);
+  DPAC_REQUIRE(weight_t);
+  DPAC_REQUIRE(save_z);
+  DPAC_REQUIRE(x);
+  DPAC_REQUIRE(dw);
+  DPAC_REQUIRE(g_gdot);
+  DPAC_REQUIRE(G);
+  if (td.sb != 0.0) DPAC_REQUIRE(u);
+  for (int i = 0; i <= net->n_hidden; ++i)
+    if (!weight_t[i]) return fail(DPAC_EINVAL, "weight_t[%d] is NULL", i);
+  dpac_mlp bnet = *net;
+  for (int i = 0; i <= net->n_hidden; ++i) bnet.weight_km[i] = weight_t_km ? weight_t_km[i] : nullptr;
+  td.x = x; td.ldx = ldx; td.u = u; td.dw = dw; td.g_gdot = g_gdot;
+  const int r = mlp_rows_bwd_launch(dtype, rows, bnet, weight_t, save_z, nullptr, G, g_x, &td,
                                     (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();
@@ -605,7 +668,8 @@ int dpac_td_assemble_fwd(const dpac_eqn_params* eq, int32_t td_type, int32_t cos
                          void* y, void* disc, void* stream) {
   if (int e = check_common(eq, dtype, num_sample)) return e;
   if (num_steps < 1) return fail(DPAC_EINVAL, "num_steps must be >= 1");
-  if (td_type != DPAC_TD1 && td_type != DPAC_TD2) return fail(DPAC_EINVAL, "bad td_type %d", td_type);
+  if (td_type != DPAC_TD1 && td_type != DPAC_TD2 && td_type != DPAC_TD1_GDOT)
+    return fail(DPAC_EINVAL, "bad td_type %d", td_type);
   if (cost_order != DPAC_COST_CRITIC && cost_order != DPAC_COST_ACTOR)
     return fail(DPAC_EINVAL, "bad cost_order %d", cost_order);
   DPAC_REQUIRE(x);
@@ -620,6 +684,7 @@ int dpac_td_assemble_fwd(const dpac_eqn_params* eq, int32_t td_type, int32_t cos
       if (int e = check_sample_type(sample_type)) return e;
     }
   }
+  if (td_type == DPAC_TD1_GDOT) DPAC_REQUIRE(G);  // gdot [N][B]; dw is not read
   OpArgs a = blank(eq, OP_TD_FWD);
   a.td_type = td_type; a.cost_order = cost_order; a.dtype = dtype; a.B = num_sample;
   a.N = num_steps; a.T = 1.0; a.x = x; a.u = u; a.dw = dw; a.seed = seed;
@@ -650,6 +715,21 @@ int dpac_td_assemble_bwd(const dpac_eqn_params* eq, int32_t dtype, int64_t num_s
   a.seed = seed; a.traj_offset = traj_offset;
   a.sample_type = sample_type == DPAC_SAMPLE_ZERO_X0 ? DPAC_SAMPLE_NORMAL : sample_type;
   a.dt_in = dt; a.coef_in = coef; a.g_y_out = g_y; a.g_G = g_G; a.stream = (hipStream_t)stream;
+  return launch(a);
+}
+
+int dpac_td_assemble_bwd_gdot(const dpac_eqn_params* eq, int32_t dtype, int64_t num_sample,
+                              int32_t num_steps, const void* dt, const void* coef, const void* g_y,
+                              void* g_gdot, void* stream) {
+  if (int e = check_common(eq, dtype, num_sample)) return e;
+  if (num_steps < 1) return fail(DPAC_EINVAL, "num_steps must be >= 1");
+  DPAC_REQUIRE(dt);
+  DPAC_REQUIRE(coef);
+  DPAC_REQUIRE(g_y);
+  DPAC_REQUIRE(g_gdot);
+  OpArgs a = blank(eq, OP_TD_BWD);
+  a.td_type = DPAC_TD1_GDOT; a.dtype = dtype; a.B = num_sample; a.N = num_steps; a.T = 1.0;
+  a.dt_in = dt; a.coef_in = coef; a.g_y_out = g_y; a.g_G = g_gdot; a.stream = (hipStream_t)stream;
   return launch(a);
 }
 

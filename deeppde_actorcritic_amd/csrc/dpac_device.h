@@ -89,6 +89,16 @@ struct Own {
 // reads 0 and drops the store whether or not the hardware counts soffset in
 // the range check: inactive lanes and padding elements need no branch.
 // ---------------------------------------------------------------------------
+// Host description of the fused TD1 operands (dpac_mlp_rows_fwd_td1 / _bwd_td1).
+struct TdRows {
+  const void *x, *u, *dw;
+  int64_t ldx;
+  int ldu, p;
+  double sa, sb;
+  void* gdot;
+  const void* g_gdot;
+};
+
 constexpr uint32_t kOOB = 0x80000000u;
 constexpr int kRsrcFlags = 0x00020000;  // gfx950 raw-buffer descriptor word 3 (guide T8)
 

@@ -835,19 +835,26 @@ struct TdArgs {
   uint64_t seed;
   const T *x, *u, *dw, *dt, *coef, *G, *g_y;
   T *y, *disc, *g_G;
+  const T* gd;  // GDOT forward: [N][B] diffusion dots from dpac_mlp_rows_fwd_td1
+  T* g_gd;      // GDOT backward: [N][B] d y / d gdot
 };
 
 template <typename T, int M, int MC, bool HAS_DW, bool HAS_G>
 struct TdFrame {
   T x[M], u[MC], dw[HAS_DW ? M : 1], G[HAS_G ? M : 1];
-  T dt, coef;
+  T dt, coef, gd;
 };
 
-template <typename T, class E, int D, bool TD1, bool PHILOX, bool BWD>
+// GDOT: the TD1 diffusion dot of each trajectory-step comes
+// precomputed from the G network's epilogue (dpac_mlp_rows_fwd_td1, bitwise the dot
+// below), so the forward reads one scalar instead of G and dw, and the backward writes
+// the scalar d y / d gdot instead of d y / d G (the G network's backward forms the
+// latter in its prologue, dpac_mlp_rows_bwd_td1) and reads neither x, u nor dw.
+template <typename T, class E, int D, bool TD1, bool PHILOX, bool BWD, bool GDOT = false>
 __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, const TdArgs<T> a) {
   constexpr int P = E::kP, M = E::M, MC = E::MC, GPW = 64 / P;
-  constexpr bool USE_DW = TD1 || BWD;
-  constexpr bool HAS_G = TD1 && !BWD;
+  constexpr bool USE_DW = (TD1 || BWD) && !GDOT;
+  constexpr bool HAS_G = TD1 && !BWD && !GDOT;
   using F = TdFrame<T, M, MC, USE_DW && !PHILOX, HAS_G>;
   constexpr int KB = ring_kb((int)sizeof(F), 3 * DPAC_RING_VGPRS, sizeof(T) == 4 ? 4 : 2);
   __shared__ T s_sum[kTdChunks][GPW];
@@ -873,7 +880,11 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
   const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(a.u, slab_u * (uint32_t)a.N);
   const __amdgpu_buffer_rsrc_t rs_dw = make_rsrc(a.dw, (USE_DW && !PHILOX) ? slab * (uint32_t)a.N : 0u);
   const __amdgpu_buffer_rsrc_t rs_G = make_rsrc(a.G, HAS_G ? slab * (uint32_t)a.N : 0u);
-  const __amdgpu_buffer_rsrc_t rs_gG = make_rsrc(a.g_G, BWD ? slab * (uint32_t)a.N : 0u);
+  const __amdgpu_buffer_rsrc_t rs_gG = make_rsrc(a.g_G, (BWD && !GDOT) ? slab * (uint32_t)a.N : 0u);
+  const uint32_t gd_bytes = (uint32_t)(B * a.N * (int64_t)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rs_gd = make_rsrc(GDOT ? (BWD ? (const T*)a.g_gd : a.gd) : nullptr,
+                                                 GDOT ? gd_bytes : 0u);
+  const uint32_t off_gd = (uint32_t)(lc.b * (int64_t)sizeof(T));  // gdot rows are [N][B]
   const __amdgpu_buffer_rsrc_t rs_dt = make_rsrc(a.dt, (uint32_t)a.B * row_bytes);
   const __amdgpu_buffer_rsrc_t rs_cf = make_rsrc(a.coef, (uint32_t)a.B * row_bytes);
   const uint32_t off_row = (uint32_t)(lc.b * row_bytes);  // dt / coef rows are [B][N]
@@ -885,10 +896,17 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
     return v;
   };
   auto load = [&](int t, F& fr) {
-    sx.load(rs_x, fr.x, (uint32_t)t * slab);
-    su.load(rs_u, fr.u, (uint32_t)t * slab_u);
+    if constexpr (!(GDOT && BWD)) {
+      sx.load(rs_x, fr.x, (uint32_t)t * slab);
+      su.load(rs_u, fr.u, (uint32_t)t * slab_u);
+    }
     if constexpr (USE_DW && !PHILOX) sx.load(rs_dw, fr.dw, (uint32_t)t * slab);
     if constexpr (HAS_G) sx.load(rs_G, fr.G, (uint32_t)t * slab);
+    if constexpr (GDOT && !BWD) {
+      uint32_t w[sizeof(T) / 4];
+      buf_load_dwords<sizeof(T) / 4>(rs_gd, off_gd, w, (uint32_t)t * (uint32_t)(B * sizeof(T)));
+      __builtin_memcpy(&fr.gd, &w[0], sizeof(T));
+    }
     fr.dt = load_scalar(rs_dt, t);
     fr.coef = load_scalar(rs_cf, t);
   };
@@ -908,7 +926,9 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
     auto body = [&](int t, F& fr, auto) {
       const T w = eq.w_finish(Lanes<P>::sum(eq.w_part(fr.x, fr.u)));
       y += cost_increment(a.cost_order, w, fr.coef, fr.dt, disc);
-      if constexpr (TD1) {
+      if constexpr (GDOT) {
+        y -= (fr.gd * disc) * (fr.coef * dsqrt(fr.dt));  // solver.py:180-184, dot precomputed
+      } else if constexpr (TD1) {
         T s[M], dwv[M];
         eq.sigma(fr.x, fr.u, s);
         increments(t, fr, dwv);
@@ -949,14 +969,19 @@ __global__ __launch_bounds__(256) void k_td(const E eq, const DevConsts<T> c, co
     disc = Dw;
     const T gy = a.g_y[lc.b];
     auto body = [&](int t, F& fr, auto) {
-      T s[M], dwv[M], out[M];
-      eq.sigma(fr.x, fr.u, s);
-      increments(t, fr, dwv);
       // d y / d G_j = -disc_t*coef_t*sqrt(dt_t)*diff_j
       const T k = -gy * (disc * (fr.coef * dsqrt(fr.dt)));
+      if constexpr (GDOT) {
+        const uint32_t off = (lc.live && lc.p == 0) ? off_gd : kOOB;
+        buf_store_scalar<T>(rs_gd, off, k, (uint32_t)t * (uint32_t)(B * sizeof(T)));
+      } else {
+        T s[M], dwv[M], out[M];
+        eq.sigma(fr.x, fr.u, s);
+        increments(t, fr, dwv);
 #pragma unroll
-      for (int m = 0; m < M; ++m) out[m] = k * (s[m] * dwv[m]);
-      sx.store(rs_gG, out, (uint32_t)t * slab);
+        for (int m = 0; m < M; ++m) out[m] = k * (s[m] * dwv[m]);
+        sx.store(rs_gG, out, (uint32_t)t * slab);
+      }
       disc = disc * disc_factor(fr.dt, fr.coef, c);
     };
     pipelined<KB, F>(t_begin, t_end, load, body);
@@ -1170,10 +1195,16 @@ int run_op(const OpArgs& a) {
       td.dt = (const T*)a.dt_in; td.coef = (const T*)a.coef_in; td.G = (const T*)a.G;
       td.g_y = (const T*)a.g_y_out;
       td.y = (T*)a.y; td.disc = (T*)a.disc; td.g_G = (T*)a.g_G;
+      td.gd = (const T*)a.G; td.g_gd = (T*)a.g_G;
       const bool philox = a.dw == nullptr;
       const dim3 tblock(64 * kTdChunks);
 #define DPAC_TD(TD1, PH, BW) hipLaunchKernelGGL((k_td<T, E, D, TD1, PH, BW>), grid, tblock, 0, s, eq, c, td)
-      if (a.op == OP_TD_BWD) {
+      if (a.td_type == DPAC_TD1_GDOT) {
+        if (a.op == OP_TD_BWD)
+          hipLaunchKernelGGL((k_td<T, E, D, true, false, true, true>), grid, tblock, 0, s, eq, c, td);
+        else
+          hipLaunchKernelGGL((k_td<T, E, D, true, false, false, true>), grid, tblock, 0, s, eq, c, td);
+      } else if (a.op == OP_TD_BWD) {
         if (philox) DPAC_TD(true, true, true); else DPAC_TD(true, false, true);
       } else if (a.td_type == DPAC_TD1) {
         if (philox) DPAC_TD(true, true, false); else DPAC_TD(true, false, false);

@@ -73,18 +73,58 @@ int64_t ws_bytes(int64_t rows, const dpac_mlp& net) {
   return nch * a.ptot * (int64_t)sizeof(T);
 }
 
+#ifndef DPAC_PG_FORK
+#define DPAC_PG_FORK 0  // narrow layers' launches on a forked stream beside the wide ones
+#endif
+// The fork: a per-device auxiliary stream and two events, created on first use (outside
+// any capture: dpac_mlp_param_grads_workspace, which every caller runs first, creates
+// them).  Inside a stream capture the event record / wait pair becomes graph edges, so
+// the narrow layers are a parallel branch of the captured graph.
+struct PgFork {
+  hipStream_t aux = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+PgFork* pg_fork() {
+  static PgFork f[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  PgFork& r = f[dev];
+  if (!r.aux) {
+    if (hipStreamCreateWithFlags(&r.aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&r.join, hipEventDisableTiming) != hipSuccess) {
+      r.aux = nullptr;
+      return nullptr;
+    }
+  }
+  return &r;
+}
+
 template <typename T>
 int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x, int64_t ldx,
-           const void* z, const void* G, void* ws, void* out, hipStream_t s) {
+           const void* z, const void* G, void* ws, void* out, hipStream_t s0) {
   PgArgs<T> a = pg_args<T>(net, rows, x, ldx, z, G);
   a.rows_per_chunk = pg_chunk_rows<T>(rows, max_ld(a));
   a.part = (T*)ws;
   const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
+  // narrow layers (K or H <= 32: grids of 256-512 small workgroups) on the forked
+  // stream; every layer writes its own partial columns, so the branches share nothing
+  PgFork* fk = DPAC_PG_FORK ? pg_fork() : nullptr;
+  bool forked = false;
   // one launch per layer: the wave grid and the tile counts are template bins
   // (wide layers: 1 x 4 waves, 2 column tiles each (f64: 1), row tiles
   // 1/2/4/8/13/16; layers of <= 32 outputs: 4 x 1 waves over the row tiles)
   for (int l = 0; l <= a.L; ++l) {
     const int K = a.width[l], H = a.width[l + 1];
+    hipStream_t s = s0;
+    if (fk && (K <= 32 || H <= 32)) {
+      if (!forked) {
+        if (hipError_t e = hipEventRecord(fk->fork, s0)) return (int)e;
+        if (hipError_t e = hipStreamWaitEvent(fk->aux, fk->fork, 0)) return (int)e;
+        forked = true;
+      }
+      s = fk->aux;
+    }
     const int nti = (K + 15) / 16;
     if (H <= 32) {
       const int ntj = (H + 15) / 16, nt4 = (nti + 3) / 4;
@@ -112,8 +152,12 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
     }
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
+  if (forked) {
+    if (hipError_t e = hipEventRecord(fk->join, fk->aux)) return (int)e;
+    if (hipError_t e = hipStreamWaitEvent(s0, fk->join, 0)) return (int)e;
+  }
   const int64_t n = a.ptot + a.width[a.L + 1];
-  hipLaunchKernelGGL(k_param_grads_reduce<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_param_grads_reduce<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s0,
                      a, (int)nch, (T)gamma_scale, (T*)out);
   return (int)hipGetLastError();
 }
@@ -144,9 +188,24 @@ MrArgs<T> mr_args(const dpac_mlp& net, int64_t rows) {
 }
 
 template <typename T>
+void set_td(MrArgs<T>& a, const TdRows* td) {
+  if (!td) return;
+  a.td_x = (const T*)td->x;
+  a.td_ldx = td->ldx;
+  a.td_u = (const T*)td->u;
+  a.td_ldu = td->ldu;
+  a.td_dw = (const T*)td->dw;
+  a.td_p = td->p;
+  a.td_sa = (T)td->sa;
+  a.td_sb = (T)td->sb;
+}
+
+template <typename T>
 int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void* out,
-             void* save_z, hipStream_t s) {
+             void* save_z, const TdRows* td, hipStream_t s) {
   MrArgs<T> a = mr_args<T>(net, rows);
+  set_td(a, td);
+  if (td) a.gdot = (T*)td->gdot;
   a.x = (const T*)x;
   a.ldx = ldx;
   a.out = (T*)out;
@@ -159,8 +218,10 @@ int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void
 
 template <typename T>
 int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const void* save_z,
-             const void* g_out, void* G, void* g_x, hipStream_t s) {
+             const void* g_out, void* G, void* g_x, const TdRows* td, hipStream_t s) {
   MrArgs<T> a = mr_args<T>(net, rows);
+  set_td(a, td);
+  if (td) a.g_gdot = (const T*)td->g_gdot;
   for (int i = 0; i <= a.L; ++i) a.wt[i] = (const T*)wt[i];
   a.z = (T*)save_z;
   a.g_out = (const T*)g_out;
@@ -175,18 +236,20 @@ int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const voi
 }  // namespace
 
 int mlp_rows_fwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx,
-                        void* out, void* save_z, hipStream_t s) {
-  return dtype == DPAC_F64 ? rows_fwd<double>(rows, net, x, ldx, out, save_z, s)
-                           : rows_fwd<float>(rows, net, x, ldx, out, save_z, s);
+                        void* out, void* save_z, const TdRows* td, hipStream_t s) {
+  return dtype == DPAC_F64 ? rows_fwd<double>(rows, net, x, ldx, out, save_z, td, s)
+                           : rows_fwd<float>(rows, net, x, ldx, out, save_z, td, s);
 }
 
 int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
-                        const void* save_z, const void* g_out, void* G, void* g_x, hipStream_t s) {
-  return dtype == DPAC_F64 ? rows_bwd<double>(rows, net, wt, save_z, g_out, G, g_x, s)
-                           : rows_bwd<float>(rows, net, wt, save_z, g_out, G, g_x, s);
+                        const void* save_z, const void* g_out, void* G, void* g_x, const TdRows* td,
+                        hipStream_t s) {
+  return dtype == DPAC_F64 ? rows_bwd<double>(rows, net, wt, save_z, g_out, G, g_x, td, s)
+                           : rows_bwd<float>(rows, net, wt, save_z, g_out, G, g_x, td, s);
 }
 
 int64_t mlp_param_grads_ws_bytes(int dtype, int64_t rows, const dpac_mlp& net) {
+  if (DPAC_PG_FORK) (void)pg_fork();
   return dtype == DPAC_F64 ? ws_bytes<double>(rows, net) : ws_bytes<float>(rows, net);
 }
 

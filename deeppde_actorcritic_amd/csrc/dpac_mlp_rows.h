@@ -21,6 +21,9 @@ constexpr int kMrThreads = 256;
 constexpr int kMrWaves = 4;
 constexpr int kMrLd = DPAC_MLP_MAX_WIDTH + 4;  // LDS row stride: 16 rows x 4 k hit 64 banks
 constexpr int kMrPrefetch = 8;
+#ifndef DPAC_MR_ROT
+#define DPAC_MR_ROT 0  // rotate the waves' column-tile sets per workgroup (timing knob)
+#endif
 #ifndef DPAC_MR_PIN
 #define DPAC_MR_PIN 0  // sched_barrier after each k group of the k-major layers (timing knob)
 #endif
@@ -59,7 +62,63 @@ struct MrArgs {
   const T* g_out;  // backward: dL/d out [rows][w_{L+1}]
   T* G;            // backward: [rows][gtot]
   T* g_x;          // backward, optional: dL/dx [rows][w_0]
+  // TD1 fused with the output layer (dpac_mlp_rows_fwd_td1 /
+  // _bwd_td1): the output G (width d) meets (sigma(x,u) dw) of its own row, with
+  // sigma_j = sa (sb == 0) or sa * (1 + (sb * x_j) * u_j) — every equation's
+  // elementwise sigma (dpac_device.h).  Components are owned as k_td owns them (lane
+  // p of a td_p-lane group: j = p*M + m) and summed with the same DPP tree, so the
+  // dot is bitwise k_td's.
+  const T* td_x;     // [rows][td_ldx] raw state rows
+  const T* td_u;     // [rows][td_ldu] (read only when sb != 0)
+  const T* td_dw;    // [rows][d]
+  int64_t td_ldx;
+  int td_ldu, td_p;
+  T td_sa, td_sb;
+  T* gdot;           // forward: [rows] sum_j (sigma_j dw_j) G_j; `out` is not written
+  const T* g_gdot;   // backward: [rows]; dL/d out_j = g_gdot * (sigma_j dw_j)
 };
+
+// (sigma(x,u) dw)_j of row r (0 past d).
+template <typename T>
+__device__ __forceinline__ T td_sdw(const MrArgs<T>& a, int64_t r, int j, int d) {
+  if (j >= d) return T(0);
+  T s = a.td_sa;
+  if (a.td_sb != T(0)) s = a.td_sa * (1 + (a.td_sb * a.td_x[r * a.td_ldx + j]) * a.td_u[r * a.td_ldu + j]);
+  return s * a.td_dw[r * d + j];
+}
+
+template <int P, typename T>
+__device__ __forceinline__ T td_group_sum(T v) {
+  return Lanes<P>::sum(v);
+}
+
+// gdot for the ROWS rows of this workgroup from the LDS image G [ROWS][kMrLd]: 16
+// lanes per row, the first td_p of them own the components (k_td's split).
+template <typename T, int ROWS>
+__device__ __forceinline__ void td_dot_rows(const MrArgs<T>& a, const T* G, int64_t row0, int rows_live,
+                                            int d, int tid) {
+  const int l16 = tid % 16, P = a.td_p, M = (d + P - 1) / P;
+  for (int rr = tid / 16; rr < ROWS; rr += kMrThreads / 16) {
+    const int64_t r = row0 + (rr < rows_live ? rr : 0);
+    T acc = T(0);
+    if (l16 < P) {
+      for (int m = 0; m < M; ++m) {
+        const int j = l16 * M + m;
+        const T g = j < d ? G[rr * kMrLd + j] : T(0);
+        const T sdw = td_sdw(a, r, j, d);
+        acc = m == 0 ? sdw * g : fma(sdw, g, acc);
+      }
+    }
+    switch (P) {
+      case 2: acc = td_group_sum<2>(acc); break;
+      case 4: acc = td_group_sum<4>(acc); break;
+      case 8: acc = td_group_sum<8>(acc); break;
+      case 16: acc = td_group_sum<16>(acc); break;
+      default: break;
+    }
+    if (l16 == 0 && rr < rows_live) a.gdot[r] = acc;
+  }
+}
 
 // acc[RT][NT] = in[RT*16 x K] @ W[K x Nout] for this wave's NT column tiles
 // (wave, wave + 4, ...), then epi.template finish<NT>(acc).  `in` is an LDS
@@ -251,6 +310,8 @@ struct MrFwdEpi {
           if (hidden) {
             yv = yv + fmax(yv, T(0));    // y + relu(y) (solver.py:269)
             lds[row * kMrLd + col] = valid ? yv : T(0);
+          } else if (!out) {             // TD1 fused: G stays in LDS
+            lds[row * kMrLd + col] = valid ? yv : T(0);
           } else if (st) {
             out[row * out_ld + col] = yv;
           }
@@ -311,12 +372,23 @@ struct MrBwdEpi {
   }
 };
 
+// The wave's column-tile set.  13 tiles over 4 waves leave one wave with 4; with
+// DPAC_MR_ROT the heavy set rotates over the workgroups that share a CU (the
+// dispatcher deals blocks round-robin over the 8 XCDs, so blocks b, b+8, ... share
+// an XCD).  Each tile is still computed by one wave in one k order: bitwise the same.
+__device__ __forceinline__ int mr_wave(int tid) {
+  int w = tid / 64;
+  if constexpr (DPAC_MR_ROT == 1) w = (w + (int)(blockIdx.x >> 3)) & (kMrWaves - 1);
+  if constexpr (DPAC_MR_ROT == 2) w = (w + (int)blockIdx.x) & (kMrWaves - 1);
+  return __builtin_amdgcn_readfirstlane(w);
+}
+
 template <typename T>
 __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_fwd(const MrArgs<T> a) {
   constexpr int RT = MrCfg<T>::RT, ROWS = RT * 16;
   __shared__ T s_img[2][ROWS * kMrLd];
   const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
+  const int wave = mr_wave(tid), lane = tid % 64;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
   const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
   const int d = a.width[0];
@@ -335,11 +407,12 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_fwd(const MrArgs<T> a) 
     MrFwdEpi<T, RT> epi{a.scale[l + 1], a.shift[l + 1], l == a.L ? a.bias : nullptr, l < a.L,
                         Nout, rows_live, s_img[pq ^ 1],
                         a.z ? a.z + row0 * a.ztot + a.zoff[l + 1] : nullptr, a.ztot,
-                        a.out + row0 * Nout, Nout};
+                        a.gdot ? nullptr : a.out + row0 * Nout, Nout};
     mr_layer<T, RT>(s_img[pq], a.width[l], Nout, a.weight[l], a.wkm[l], wave, lane, epi);
     __syncthreads();
     pq ^= 1;
   }
+  if (a.gdot) td_dot_rows<T, ROWS>(a, s_img[pq], row0, rows_live, a.width[a.L + 1], tid);
 }
 
 template <typename T>
@@ -347,7 +420,7 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_bwd(const MrArgs<T> a) 
   constexpr int RT = MrCfg<T>::RT, ROWS = RT * 16;
   __shared__ T s_img[2][ROWS * kMrLd];
   const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
+  const int wave = mr_wave(tid), lane = tid % 64;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS;
   const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
   const int L = a.L, hout = a.width[L + 1];
@@ -356,7 +429,8 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_bwd(const MrArgs<T> a) 
     const int r = e / kMrLd, k = e % kMrLd;
     T v = T(0);
     if (k < hout && r < rows_live) {
-      v = a.g_out[(row0 + r) * hout + k];
+      v = a.g_gdot ? a.g_gdot[row0 + r] * td_sdw(a, row0 + r, k, hout)  // td_assemble_bwd's product
+                   : a.g_out[(row0 + r) * hout + k];
       a.G[(row0 + r) * a.gtot + a.goff[L + 1] + k] = v;
     }
     s_img[0][e] = v;

@@ -529,6 +529,78 @@ def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, w
     return g_x, grads
 
 
+# ---- the critic's G network with the TD1 dot fused ----
+# "fused": critic_front runs dpac_mlp_rows_fwd_td1 (G never reaches HBM, only the
+# per-step dots), the TD assembly reads those dots (DPAC_TD1_GDOT), and the G
+# backward forms dL/dG in its prologue (dpac_mlp_rows_bwd_td1); "split": G [N*B, d]
+# and dL/dG are written and read (dpac_mlp_rows_fwd + dpac_td_assemble_fwd/_bwd).
+# Both give bitwise the same y, disc and gradients (tests/test_gpu_td_fused.py).
+CRITIC_TD1 = os.environ.get("DPAC_CRITIC_TD1", "fused")
+if CRITIC_TD1 not in ("fused", "split"):
+    raise ValueError(f"DPAC_CRITIC_TD1 must be 'fused' or 'split', got {CRITIC_TD1!r}")
+
+
+def mlp_rows_td1(eqp, view: MlpView, x: torch.Tensor, u: torch.Tensor, dw: torch.Tensor,
+                 save: bool = False):
+    """gdot [R] = Σ_j (σ(x,u)·dw)_j · G_j(x) for G = the network (width d in and out)
+    over the rows x [R, d] (solver.py:179-184 without G ever written), one
+    dpac_mlp_rows_fwd_td1 launch; u [R, c] and dw [R, d] row-aligned with x.  With
+    save=True also the backward saves z [R, Σ widths[1:]]."""
+    _require_gpu(x, u, dw, *view.tensors)
+    _check_same(x, u, dw, *view.tensors)
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("mlp_rows_td1: x must be [rows, d] with unit column stride")
+    R = x.shape[0]
+    if u.shape[0] != R or dw.shape != (R, eqp.dim):
+        raise ValueError("mlp_rows_td1: u [R, c] and dw [R, d] must be row-aligned with x")
+    gdot = torch.empty(R, dtype=x.dtype, device=x.device)
+    z = torch.empty(R, sum(view.widths[1:]), dtype=x.dtype, device=x.device) if save else None
+    call("dpac_mlp_rows_fwd_td1", ctypes.byref(eqp), _dtype_id(x), R, ctypes.byref(view.struct),
+         ctypes.c_void_p(x.data_ptr()), x.stride(0), _ptr(u.contiguous()), _ptr(dw.contiguous()),
+         _ptr(gdot), _ptr(z), _stream(x))
+    return gdot, z
+
+
+def td_assemble_gdot(eqp, x, u, dt, coef, gdot, *, cost_order: int = _lib.COST_CRITIC):
+    """(y [B], disc_N [B]) of TD1 from the fused dots gdot [N, B] (DPAC_TD1_GDOT; no
+    autograd: the critic's split step differentiates by hand)."""
+    _require_gpu(x, u, dt, coef, gdot)
+    B, N = dt.shape
+    y = torch.empty(B, dtype=x.dtype, device=x.device)
+    disc = torch.empty_like(y)
+    call("dpac_td_assemble_fwd", ctypes.byref(eqp), _lib.TD1_GDOT, cost_order, _dtype_id(x), B, N,
+         _ptr(x.contiguous()), _ptr(u.contiguous()), None, 0, 0, _lib.SAMPLE_NORMAL,
+         _ptr(dt.contiguous()), _ptr(coef.contiguous()), _ptr(gdot.contiguous()), _ptr(y),
+         _ptr(disc), _stream(x))
+    return y, disc
+
+
+def td_assemble_bwd_gdot(eqp, dt, coef, g_y):
+    """d L / d gdot [N, B] = −g_y·disc_t·coef_t·√dt_t given dL/dy [B]."""
+    _require_gpu(dt, coef, g_y)
+    B, N = dt.shape
+    g_gdot = torch.empty(N, B, dtype=dt.dtype, device=dt.device)
+    call("dpac_td_assemble_bwd_gdot", ctypes.byref(eqp), _dtype_id(dt), B, N,
+         _ptr(dt.contiguous()), _ptr(coef.contiguous()), _ptr(g_y.contiguous()), _ptr(g_gdot),
+         _stream(dt))
+    return g_gdot
+
+
+def row_mlp_backward_td1(eqp, rs, params, x, z, u, dw, g_gdot, want_params: bool = True,
+                         ws_tag: int = 0):
+    """row_mlp_backward for mlp_rows_td1: dpac_mlp_rows_bwd_td1 (dL/dG = g_gdot·σ dw in
+    its prologue) then dpac_mlp_param_grads; returns the parameter gradients."""
+    L, gam, bet, Ws, b = _split_params(params)
+    view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, False, True)
+    R = x.shape[0]
+    G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
+    call("dpac_mlp_rows_bwd_td1", ctypes.byref(eqp), _dtype_id(x), R, ctypes.byref(view.struct),
+         _ptr_array(wt), _ptr_array(wt_km), _ptr(z), ctypes.c_void_p(x.data_ptr()), x.stride(0),
+         _ptr(u.contiguous()), _ptr(dw.contiguous()), _ptr(g_gdot.contiguous()), _ptr(G), None,
+         _stream(x))
+    return mlp_param_grads(view, x, z, G, params, ws_tag) if want_params else None
+
+
 def row_mlp(net, x: torch.Tensor, const_params: bool = False) -> torch.Tensor:
     """net(x) before the Eikonal head, x [..., d] -> [..., w_out], through the kernels.
     const_params: the parameters are constants for autograd (only dL/dx is formed),

@@ -641,9 +641,16 @@ class ActorCriticSolver(object):
             x, dt, coef, u = self.bsde.rollout(mc.scheme, d.x0, d.dw, T, N, self.model_actor.NN_control,
                                                cheat=self.cheat_control_in_critic)
             rows = x[:N].reshape(N * B, -1)
-            G, zG = ops.mlp_rows(Gnet.mlp_view(), rows, save=True)
-            y, disc = ops.td_assemble(eqp, mc.td, x, u, d.dw, dt, coef, G.view(N, B, -1),
-                                      cost_order=_lib.COST_CRITIC)
+            fused = ops.CRITIC_TD1 == "fused"
+            if fused:  # G never written, only its TD1 dots
+                u_rows, dw_rows = u.reshape(N * B, -1), d.dw.reshape(N * B, -1)
+                gdot, zG = ops.mlp_rows_td1(eqp, Gnet.mlp_view(), rows, u_rows, dw_rows, save=True)
+                y, disc = ops.td_assemble_gdot(eqp, x, u, dt, coef, gdot.view(N, B),
+                                               cost_order=_lib.COST_CRITIC)
+            else:
+                G, zG = ops.mlp_rows(Gnet.mlp_view(), rows, save=True)
+                y, disc = ops.td_assemble(eqp, mc.td, x, u, d.dw, dt, coef, G.view(N, B, -1),
+                                          cost_order=_lib.COST_CRITIC)
             xv = torch.cat([x[0], x[N], d.x_bdry])
             Vout, zV = ops.mlp_rows(Vnet.mlp_view(), xv, save=True)
             V = Vout[:, 0]
@@ -654,15 +661,23 @@ class ActorCriticSolver(object):
             g_out = torch.cat([g, -g * disc, g_b]).unsqueeze(1)
             _, gV = ops.row_mlp_backward(Vnet.bn_rs, Vnet.trainable_variables(), xv, zV, g_out,
                                          False, True)
+            if fused:
+                g_gdot = ops.td_assemble_bwd_gdot(eqp, dt, coef, -g)
+                return gV, g_gdot.reshape(N * B), rows, zG, u_rows, dw_rows
             gG = ops.td_assemble_bwd(eqp, x, u, d.dw, dt, coef, -g)
         return gV, gG.reshape(N * B, -1), rows, zG
 
     def critic_G_back(self, front):
-        """G's parameter gradients from critic_front's outputs (dpac_mlp_rows_bwd +
+        """G's parameter gradients from critic_front's outputs (dpac_mlp_rows_bwd[_td1] +
         dpac_mlp_param_grads, on their own scratch buffer: they run beside the BPTT)."""
-        _, gG, rows, z = front
         net = self.model_critic.NN_value_grad
         with torch.no_grad():
+            if len(front) == 6:  # fused TD1: dL/dG formed from dL/dgdot in the prologue
+                _, g_gdot, rows, z, u_rows, dw_rows = front
+                return ops.row_mlp_backward_td1(self.bsde.params(), net.bn_rs,
+                                                net.trainable_variables(), rows, z, u_rows,
+                                                dw_rows, g_gdot, True, ws_tag=1)
+            _, gG, rows, z = front
             _, grads = ops.row_mlp_backward(net.bn_rs, net.trainable_variables(), rows, z, gG,
                                             False, True, ws_tag=1)
         return grads

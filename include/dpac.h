@@ -73,6 +73,7 @@ extern "C" {
 /* TD targets — solver.py:177 ("TD1" = VR-LSTD with the G control variate; "TD2" = LSTD) */
 #define DPAC_TD1 1
 #define DPAC_TD2 2
+#define DPAC_TD1_GDOT 3 /* TD1 with the diffusion dot precomputed (dpac_mlp_rows_fwd_td1) */
 
 /* cost-accumulation order: the critic (solver.py:170-174) and the actor
  * (solver.py:218) multiply the same four factors in different orders */
@@ -194,7 +195,10 @@ int dpac_step_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
  * this is the actor's pathwise cost without the terminal value
  * (solver.py:213-219): dpac_actor_cost_fwd is that alias.
  * dw may be NULL → regenerated from the Philox stream (seed, traj_offset,
- * sample_type) exactly as dpac_sample / dpac_rollout_fwd drew it. */
+ * sample_type) exactly as dpac_sample / dpac_rollout_fwd drew it.
+ * td_type = DPAC_TD1_GDOT: TD1 with G holding gdot [N][B], the per-step dots
+ * Σ_j (σ(x_t,u_t)dw_t)_j·G_j(x_t) written by dpac_mlp_rows_fwd_td1; dw is not read.
+ * y and disc are bitwise those of DPAC_TD1 on the same G. */
 int dpac_td_assemble_fwd(const dpac_eqn_params* eq, int32_t td_type,
                          int32_t cost_order, int32_t dtype, int64_t num_sample,
                          int32_t num_steps, const void* x, const void* u,
@@ -210,6 +214,13 @@ int dpac_td_assemble_bwd(const dpac_eqn_params* eq, int32_t dtype,
                          int64_t traj_offset, int32_t sample_type,
                          const void* dt, const void* coef, const void* g_y,
                          void* g_G, void* stream);
+
+/* d y / d gdot for DPAC_TD1_GDOT: g_gdot[t][b] = −g_y[b]·disc_t·coef_t·√dt_t (reads
+ * only dt, coef and g_y); dpac_mlp_rows_bwd_td1 turns it into d y / d G. */
+int dpac_td_assemble_bwd_gdot(const dpac_eqn_params* eq, int32_t dtype,
+                              int64_t num_sample, int32_t num_steps, const void* dt,
+                              const void* coef, const void* g_y, void* g_gdot,
+                              void* stream);
 
 /* ActorModel pathwise cost without the terminal term (solver.py:213-219). */
 int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
@@ -328,6 +339,26 @@ int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
 int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* const* weight_t,
                       const void* const* weight_t_km, const void* save_z, const void* g_out, void* G,
                       void* g_x, void* stream);
+
+/* ---- the G network with the TD1 dot fused ---------
+ * solver.py:179-184 evaluates G = NN_value_grad(x_t) and immediately dots it with
+ * σ(x_t,u_t)dw_t.  dpac_mlp_rows_fwd_td1 runs the network (width[0] = width[L+1]
+ * = d) over the rollout rows x [rows][ldx] (rows = N·B, step-major, as x[:N]) and
+ * writes only gdot[r] = Σ_j (σ(x_r,u_r)dw_r)_j·G_j(x_r) — G itself never reaches
+ * HBM — plus the optional backward saves.  u [rows][control_dim] is read only for
+ * LQR_var (state-dependent σ, equation.py:302); dw [rows][d].  gdot is bitwise the
+ * dot dpac_td_assemble_fwd(DPAC_TD1) forms from the same G.
+ * dpac_mlp_rows_bwd_td1 is dpac_mlp_rows_bwd with dL/d out = g_gdot[r]·(σ dw)_r,
+ * formed in its prologue (bitwise dpac_td_assemble_bwd's d y / d G times the same
+ * upstream gradient). */
+int dpac_mlp_rows_fwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows,
+                          const dpac_mlp* net, const void* x, int64_t ldx, const void* u,
+                          const void* dw, void* gdot, void* save_z, void* stream);
+int dpac_mlp_rows_bwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows,
+                          const dpac_mlp* net, const void* const* weight_t,
+                          const void* const* weight_t_km, const void* save_z, const void* x,
+                          int64_t ldx, const void* u, const void* dw, const void* g_gdot,
+                          void* G, void* g_x, void* stream);
 
 /* ---- parameter gradients of a dpac_mlp over independent rows -------------
  * What GradientTape returns for DeepNN's trainable variables (solver.py:88,95

@@ -48,6 +48,7 @@ def test_constants_match_header():
              "DPAC_EQN_VDP": _lib.EQN_VDP, "DPAC_EQN_EKN": _lib.EQN_EKN,
              "DPAC_EQN_LQR_VAR": _lib.EQN_LQR_VAR, "DPAC_SCHEME_NAIVE": _lib.SCHEME_NAIVE,
              "DPAC_SCHEME_ADAPTIVE": _lib.SCHEME_ADAPTIVE, "DPAC_TD1": _lib.TD1, "DPAC_TD2": _lib.TD2,
+             "DPAC_TD1_GDOT": _lib.TD1_GDOT,
              "DPAC_COST_CRITIC": _lib.COST_CRITIC, "DPAC_COST_ACTOR": _lib.COST_ACTOR,
              "DPAC_SAMPLE_NORMAL": _lib.SAMPLE_NORMAL, "DPAC_SAMPLE_BOUNDED": _lib.SAMPLE_BOUNDED,
              "DPAC_SAMPLE_ZERO_X0": _lib.SAMPLE_ZERO_X0, "DPAC_EVAL_B": _lib.EVAL_B,
@@ -83,6 +84,18 @@ def test_supported_dims():
     assert lib.dpac_supported(None) == 0
 
 
+def _net(d_in, d_out, hidden=32):
+    """A dpac_mlp with dummy (never dereferenced) pointers: host validation only."""
+    n = _lib.Mlp()
+    n.n_hidden = 1
+    n.width[0], n.width[1], n.width[2] = d_in, hidden, d_out
+    for i in range(3):
+        n.bn_scale[i] = n.bn_shift[i] = 0x1000
+    n.weight[0] = n.weight[1] = 0x1000
+    n.bias = 0x1000
+    return n
+
+
 def test_validation_without_gpu():
     """Bad arguments are rejected on the host with DPAC_EINVAL and a message."""
     p = _params()
@@ -110,6 +123,17 @@ def test_validation_without_gpu():
                            dummy, dummy, None, None, None, None, None), "alias"),
         ("dpac_sample", (ctypes.byref(p), 5, 0, 16, 10, 1, 0, dummy, dummy, dummy, None), "sample_type"),
         ("dpac_equation_eval", (ctypes.byref(p), 99, 0, 16, dummy, dummy, dummy, None), "eval"),
+        # fused TD1: the G network's widths must be d
+        ("dpac_mlp_rows_fwd_td1", (ctypes.byref(p), 0, 64, ctypes.byref(_net(20, 16)), dummy, 20, dummy,
+                                   dummy, dummy, None, None), "output width"),
+        ("dpac_mlp_rows_fwd_td1", (ctypes.byref(p), 0, 64, ctypes.byref(_net(20, 20)), dummy, 20, dummy,
+                                   dummy, None, None, None), "gdot"),
+        ("dpac_mlp_rows_bwd_td1", (ctypes.byref(p), 0, 64, ctypes.byref(_net(20, 20)), None, None, dummy,
+                                   dummy, 20, dummy, dummy, dummy, dummy, None, None), "weight_t"),
+        ("dpac_td_assemble_bwd_gdot", (ctypes.byref(p), 0, 16, 10, dummy, dummy, None, dummy, None),
+         "g_y"),
+        ("dpac_td_assemble_fwd", (ctypes.byref(p), _lib.TD1_GDOT, 0, 0, 16, 10, dummy, dummy, None, 0, 0,
+                                  0, dummy, dummy, None, dummy, dummy, None), "G"),
     ]
     for name, args, word in cases:
         with pytest.raises(_lib.DpacError) as ei:
