@@ -500,7 +500,7 @@ int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
 }
 
 // The equation's elementwise sigma as (sa, sb) and k_td's lane split, for the fused
-// TD1 entry points (dpac_mlp_rows.h: TdRows).
+// TD1 entry points (TdRows, dpac_device.h; used by dpac_mlp_rows.h).
 static int td_rows_setup(const dpac_eqn_params* eq, int32_t dtype, int64_t rows, const dpac_mlp* net,
                          dpac::TdRows& td) {
   if (int e = check_common(eq, dtype, rows)) return e;

@@ -94,19 +94,44 @@ __device__ __forceinline__ T td_group_sum(T v) {
 
 // gdot for the ROWS rows of this workgroup from the LDS image G [ROWS][kMrLd]: 16
 // lanes per row, the first td_p of them own the components (k_td's split).
+// With one row per 16 lanes (ROWS == 16) and at most kTdPre components per lane, the
+// lane's (sigma dw) values are loaded at kernel start (td_prefetch), so the dot phase
+// after the last layer reads only LDS.
+constexpr int kTdPre = 4;
+template <typename T, int ROWS>
+__device__ __forceinline__ bool td_prefetch(const MrArgs<T>& a, int64_t row0, int rows_live, int d, int tid,
+                                            T (&pre)[kTdPre]) {
+  const int P = a.td_p, M = (d + P - 1) / P;
+  if (!a.gdot || ROWS != kMrThreads / 16 || M > kTdPre) return false;
+  const int l16 = tid % 16, rr = tid / 16;
+  const int64_t r = row0 + (rr < rows_live ? rr : 0);
+#pragma unroll
+  for (int m = 0; m < kTdPre; ++m) pre[m] = (l16 < P && m < M) ? td_sdw(a, r, l16 * M + m, d) : T(0);
+  return true;
+}
+
 template <typename T, int ROWS>
 __device__ __forceinline__ void td_dot_rows(const MrArgs<T>& a, const T* G, int64_t row0, int rows_live,
-                                            int d, int tid) {
+                                            int d, int tid, bool have_pre, const T (&pre)[kTdPre]) {
   const int l16 = tid % 16, P = a.td_p, M = (d + P - 1) / P;
   for (int rr = tid / 16; rr < ROWS; rr += kMrThreads / 16) {
     const int64_t r = row0 + (rr < rows_live ? rr : 0);
     T acc = T(0);
     if (l16 < P) {
-      for (int m = 0; m < M; ++m) {
-        const int j = l16 * M + m;
-        const T g = j < d ? G[rr * kMrLd + j] : T(0);
-        const T sdw = td_sdw(a, r, j, d);
-        acc = m == 0 ? sdw * g : fma(sdw, g, acc);
+      if (have_pre) {
+#pragma unroll
+        for (int m = 0; m < kTdPre; ++m) {
+          const int j = l16 * M + m;
+          const T g = (m < M && j < d) ? G[rr * kMrLd + j] : T(0);
+          if (m < M) acc = m == 0 ? pre[m] * g : fma(pre[m], g, acc);
+        }
+      } else {
+        for (int m = 0; m < M; ++m) {
+          const int j = l16 * M + m;
+          const T g = j < d ? G[rr * kMrLd + j] : T(0);
+          const T sdw = td_sdw(a, r, j, d);
+          acc = m == 0 ? sdw * g : fma(sdw, g, acc);
+        }
       }
     }
     switch (P) {
@@ -400,6 +425,8 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_fwd(const MrArgs<T> a) 
     s_img[0][e] = v;
     s_img[1][e] = T(0);
   }
+  T td_pre[kTdPre];
+  const bool have_pre = td_prefetch<T, ROWS>(a, row0, rows_live, a.width[a.L + 1], tid, td_pre);
   __syncthreads();
   int pq = 0;
   for (int l = 0; l <= a.L; ++l) {
@@ -412,7 +439,7 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_fwd(const MrArgs<T> a) 
     __syncthreads();
     pq ^= 1;
   }
-  if (a.gdot) td_dot_rows<T, ROWS>(a, s_img[pq], row0, rows_live, a.width[a.L + 1], tid);
+  if (a.gdot) td_dot_rows<T, ROWS>(a, s_img[pq], row0, rows_live, a.width[a.L + 1], tid, have_pre, td_pre);
 }
 
 template <typename T>
