@@ -12,6 +12,7 @@ run 300 bench python bench.py --steps 200 --warmup 20
 run 200 probe_bptt python -u tools/probe_bptt.py --B 2048,4096 --N 100
 run 300 train2k python -u tools/train_bench.py --iters 20 --batch 2048
 run 300 train4k python -u tools/train_bench.py --iters 20 --batch 4096
+run 200 probe_td_fused python -u tools/probe_td_fused.py 2048 4096
 run 300 prof_kt rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-train
 run 300 prof_train rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_train -o run --output-format csv -- python tools/train_bench.py --iters 3 --warmup 1 --dtype float32
 run 300 pmc_fetch rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
