@@ -476,14 +476,23 @@ struct StagedPlan {
   static constexpr int TPW = kStCW * (64 / P);                                   // trajectories per workgroup
   static constexpr int SLOT = TPW * D * (int)sizeof(T);                          // bytes of one step's rows
   static constexpr int PIECES = (SLOT + 1023) / 1024;                            // 1 KB DMA instructions per step
-  static constexpr int SLOT_LDS = (SLOT + 16 + 1023) / 1024 * 1024;              // + a zero pad no DMA writes
-  static constexpr int PADOFF = SLOT_LDS - 16;                                   // where empty lanes read 0
   // ring depth (steps): the loader publishes a chunk once the next one is issued, so it
   // needs >= 2 chunks; 4 keep it far enough ahead that the compute waves never wait
-  // (measured at B = 4096, cold: 4 chunks 29.3 us, 2 chunks 41.6, k_rollout 38.3); where 4
-  // chunks do not fit in 128 KB (float64 at d = 20) k_rollout runs instead
-  static constexpr int RS = DPAC_ST_CHUNKS * kStCH;
-  static constexpr bool kOk = P >= 4 && RS * SLOT_LDS <= 128 * 1024 && kStCH * PIECES <= 62;
+  // (measured at B = 4096, cold: 4 chunks 29.3 us, 2 chunks 41.6, k_rollout 38.3).  Slots
+  // are 1 KB-aligned when 4 chunks of them fit in 128 KB; otherwise (float64 at d = 20:
+  // 2560-byte slots) 3 chunks of 16-byte-aligned slots (121 KB) — every DMA piece still
+  // starts inside its slot and the lane-0 filler write (at k*1024 < SLOT) never reaches
+  // the pad.  Plans that fit neither way run k_rollout.
+  static constexpr int kLdsCap = 128 * 1024;
+  static constexpr int SLOT_1K = (SLOT + 16 + 1023) / 1024 * 1024;
+  static constexpr int SLOT_16 = (SLOT + 16 + 15) / 16 * 16;
+  static constexpr bool kWide = DPAC_ST_CHUNKS * kStCH * SLOT_1K <= kLdsCap;
+  static constexpr int CHUNKS = kWide ? DPAC_ST_CHUNKS : 3;
+  static constexpr int SLOT_LDS = kWide ? SLOT_1K : SLOT_16;  // + a zero pad no DMA writes
+  static constexpr int PADOFF = SLOT_LDS - 16;                 // where empty lanes read 0
+  static constexpr int RS = CHUNKS * kStCH;
+  static_assert(P < 4 || (SLOT % 16 == 0 && (PIECES - 1) * 1024 + 16 <= SLOT), "DMA pieces stay inside the slot");
+  static constexpr bool kOk = P >= 4 && RS * SLOT_LDS <= kLdsCap && kStCH * PIECES <= 62;
 };
 
 template <class Fn, int... S>
