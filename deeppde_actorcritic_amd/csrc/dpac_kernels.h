@@ -469,6 +469,12 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
 #ifndef DPAC_ST_CHUNKS
 #define DPAC_ST_CHUNKS 4  // hand-off chunks in the LDS ring
 #endif
+#ifndef DPAC_ST_TIGHT
+#define DPAC_ST_TIGHT 0  // timing knob: 16-byte-aligned slots for every plan
+#endif
+#ifndef DPAC_ST_TIGHT_CHUNKS
+#define DPAC_ST_TIGHT_CHUNKS 3  // hand-off chunks of a ring of 16-byte-aligned slots
+#endif
 constexpr int kStCW = 4;   // compute wavefronts per workgroup
 constexpr int kStCH = 16;  // steps per hand-off chunk
 template <typename T, int D, int P>
@@ -486,8 +492,8 @@ struct StagedPlan {
   static constexpr int kLdsCap = 128 * 1024;
   static constexpr int SLOT_1K = (SLOT + 16 + 1023) / 1024 * 1024;
   static constexpr int SLOT_16 = (SLOT + 16 + 15) / 16 * 16;
-  static constexpr bool kWide = DPAC_ST_CHUNKS * kStCH * SLOT_1K <= kLdsCap;
-  static constexpr int CHUNKS = kWide ? DPAC_ST_CHUNKS : 3;
+  static constexpr bool kWide = !DPAC_ST_TIGHT && DPAC_ST_CHUNKS * kStCH * SLOT_1K <= kLdsCap;
+  static constexpr int CHUNKS = kWide ? DPAC_ST_CHUNKS : DPAC_ST_TIGHT_CHUNKS;
   static constexpr int SLOT_LDS = kWide ? SLOT_1K : SLOT_16;  // + a zero pad no DMA writes
   static constexpr int PADOFF = SLOT_LDS - 16;                 // where empty lanes read 0
   static constexpr int RS = CHUNKS * kStCH;
