@@ -30,9 +30,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--config", default="lqr_d20", help="a BASELINE config: lqr_d20, ekn_d20, lqr_var_d20, vdp_d20")
     a = ap.parse_args()
-    cfg = lqr_d20(a.iters, 10 ** 9, a.dtype, a.batch, a.batch)
-    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=1, sampler="device")
+    cfg = lqr_d20(a.iters, 10 ** 9, a.dtype, a.batch, a.batch, name=a.config)
+    sp = psol.ActorCriticSolver(cfg, getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config), seed=1,
+                                sampler="device")
     B, N = a.batch, cfg.eqn_config.num_time_interval_critic
 
     def critic():
@@ -67,7 +69,7 @@ def main():
         ta += t2 - t1
         ti += t3 - t2
     ms = ti / a.iters * 1e3
-    print(json.dumps({"config": "lqr_d20", "dtype": a.dtype, "batch": B, "N": N, "iters": a.iters,
+    print(json.dumps({"config": a.config, "dtype": a.dtype, "batch": B, "N": N, "iters": a.iters,
                       "ms_per_iter": ms, "sequential_ms": (tc + ta) / a.iters * 1e3,
                       "critic_ms": tc / a.iters * 1e3, "actor_ms": ta / a.iters * 1e3,
                       "traj_steps_per_s": 2 * B * N / (ms * 1e-3)}), flush=True)
