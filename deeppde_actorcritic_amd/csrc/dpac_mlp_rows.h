@@ -19,7 +19,10 @@ namespace dpac {
 
 constexpr int kMrThreads = 256;
 constexpr int kMrWaves = 4;
-constexpr int kMrLd = DPAC_MLP_MAX_WIDTH + 4;  // LDS row stride: 16 rows x 4 k hit 64 banks
+#ifndef DPAC_MR_LD_PAD
+#define DPAC_MR_LD_PAD 8  // row stride 264 = 8 mod 64 dwords: conflict-free ds_read_b128 A reads on gfx950 (+4 left 2-way conflicts)
+#endif
+constexpr int kMrLd = DPAC_MLP_MAX_WIDTH + DPAC_MR_LD_PAD;  // LDS row stride: 16 rows x 4 k hit 64 banks
 constexpr int kMrPrefetch = 8;
 #ifndef DPAC_MR_ROT
 #define DPAC_MR_ROT 0  // rotate the waves' column-tile sets per workgroup (timing knob)

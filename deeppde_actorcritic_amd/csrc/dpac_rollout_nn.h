@@ -25,7 +25,10 @@
 constexpr int kNnRows = 16;  // trajectories per workgroup = one MFMA row tile
 constexpr int kNnWaves = DPAC_NN_WAVES;
 constexpr int kNnThreads = 64 * kNnWaves;
-constexpr int kNnLd = DPAC_MLP_MAX_WIDTH + 4;  // LDS row stride (elements)
+#ifndef DPAC_NN_LD_PAD
+#define DPAC_NN_LD_PAD 4  // LDS row stride = max width + pad (elements)
+#endif
+constexpr int kNnLd = DPAC_MLP_MAX_WIDTH + DPAC_NN_LD_PAD;  // LDS row stride (elements)
 constexpr int kNnMaxTilesPerWave = (DPAC_MLP_MAX_WIDTH / 16 + kNnWaves - 1) / kNnWaves;
 #ifndef DPAC_NN_PREFETCH
 #define DPAC_NN_PREFETCH 4  // measured 14.9 -> 14.7 us per step (12, 16: slower)
