@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPAC_LIB", os.path.join(_HERE, "libdpac.so"))
 
 # constants mirrored from include/dpac.h
+ABI_VERSION = 2  # DPAC_ABI_VERSION: load() refuses a library built from another header
 DPAC_OK, DPAC_EINVAL, DPAC_EUNSUP = 0, -1, -2
 F32, F64 = 0, 1
 EQN_LQR, EQN_VDP, EQN_EKN, EQN_LQR_VAR = 0, 1, 2, 3
@@ -95,6 +96,7 @@ SIGNATURES = {
                             ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), _P, _P,
                             _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "dpac_rollout_nn_mask_tile_bytes": [ctypes.POINTER(Mlp)],
+    "dpac_rollout_nn_mask_bytes": [ctypes.POINTER(Mlp), _I32, _I64, _I32],
     "dpac_rollout_nn_fwd_masked": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp), _P, _P, _P, _P,
                                    _P, _P, _I32, _P, _P, _P, _P, _P, _P, ctypes.POINTER(_I32), _P],
     "dpac_rollout_nn_bwd_masked": [_EQ, _I32, _I32, _I64, _I32, _D, ctypes.POINTER(Mlp),
@@ -115,7 +117,8 @@ SIGNATURES = {
                         ctypes.POINTER(ctypes.c_void_p), _D, _D, _D, _D, _P],
 }
 _RESTYPES = {"dpac_abi_version": ctypes.c_int32, "dpac_last_error": ctypes.c_char_p,
-             "dpac_supported": ctypes.c_int32, "dpac_mlp_param_grads_workspace": ctypes.c_int64}
+             "dpac_supported": ctypes.c_int32, "dpac_mlp_param_grads_workspace": ctypes.c_int64,
+             "dpac_rollout_nn_mask_tile_bytes": ctypes.c_int32, "dpac_rollout_nn_mask_bytes": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None
@@ -139,6 +142,19 @@ def load() -> ctypes.CDLL:
         except OSError as e:  # pragma: no cover - depends on the host
             _load_error = f"failed to load {LIB_PATH}: {e}"
             raise DpacUnavailable(_load_error) from e
+        # check the version before binding anything: a library built from another header
+        # (e.g. a stale DPAC_LIB build) would take shifted arguments
+        try:
+            ver_fn = lib.dpac_abi_version
+        except AttributeError as e:
+            _load_error = f"{LIB_PATH} does not export dpac_abi_version: not a libdpac build"
+            raise DpacUnavailable(_load_error) from e
+        ver_fn.argtypes, ver_fn.restype = [], ctypes.c_int32
+        ver = int(ver_fn())
+        if ver != ABI_VERSION:
+            _load_error = (f"{LIB_PATH} has DPAC_ABI_VERSION {ver}, these bindings need {ABI_VERSION}: "
+                           "rebuild it with `make lib`")
+            raise DpacUnavailable(_load_error)
         for name, argtypes in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.argtypes = argtypes

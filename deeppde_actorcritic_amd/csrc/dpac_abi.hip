@@ -369,6 +369,21 @@ int32_t dpac_rollout_nn_mask_tile_bytes(const dpac_mlp* actor) {
   return nn_mask_tile_bytes(actor->n_hidden);
 }
 
+int64_t dpac_rollout_nn_mask_bytes(const dpac_mlp* actor, int32_t dtype, int64_t num_sample,
+                                   int32_t num_steps) {
+  if (!actor || actor->n_hidden < 1 || actor->n_hidden > DPAC_MLP_MAX_HIDDEN || num_sample < 1 ||
+      num_steps < 1 || (dtype != DPAC_F32 && dtype != DPAC_F64))
+    return fail(DPAC_EINVAL, "dpac_rollout_nn_mask_bytes: bad arguments"), -1;
+  ok();
+  // the same selection as run_op's OP_ROLLOUT_NN: float, 16-row tiles, the fast path
+  if (dtype != DPAC_F32) return 0;
+  const int tile = nn_tile_rows();
+  if (tile == 4 || (tile == 0 && num_sample <= 1024)) return 0;
+  const int L = actor->n_hidden;
+  if (!nn_fast_host<float>(L, actor->width, actor->weight_km, actor->width[0], actor->width[L + 1])) return 0;
+  return (int64_t)num_steps * ((num_sample + 15) / 16) * nn_mask_tile_bytes(L);
+}
+
 int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
                         int64_t num_sample, int32_t num_steps, double total_time,
                         const dpac_mlp* actor, const void* x0, const void* dw, void* x,
@@ -500,20 +515,28 @@ int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
 }
 
 // The equation's elementwise sigma as (sa, sb) and k_td's lane split, for the fused
-// TD1 entry points (TdRows, dpac_device.h; used by dpac_mlp_rows.h).
+// TD1 entry points (TdRows, dpac_device.h; used by dpac_mlp_rows.h).  Both come from the
+// equation functors themselves (E::sigma_form, eqn_lanes), over an explicit allow-list of
+// equation ids, so a new equation cannot reach the fused path with another's sigma.
 static int td_rows_setup(const dpac_eqn_params* eq, int32_t dtype, int64_t rows, const dpac_mlp* net,
                          dpac::TdRows& td) {
   if (int e = check_common(eq, dtype, rows)) return e;
   if (int e = check_net(net)) return e;
+  if (net->ekn_head) return fail(DPAC_EINVAL, "the fused TD1 G network takes no Eikonal head");
   const int d = eq->dim;
   if (net->width[net->n_hidden + 1] != d)
     return fail(DPAC_EINVAL, "the network's output width (%d) must equal dim (%d)",
                 net->width[net->n_hidden + 1], d);
   if (net->width[0] != d)
     return fail(DPAC_EINVAL, "the network's input width (%d) must equal dim (%d)", net->width[0], d);
-  td.p = eq->eqn == DPAC_EQN_VDP ? 1 : lanes_for_dim(d);  // E::kP of the equation's k_td
-  td.sa = 1.4142135623730951;                               // np.sqrt(2.0) (equation.py:170)
-  td.sb = eq->eqn == DPAC_EQN_LQR_VAR ? eq->epsilon : 0.0;  // LQR_var: sqrt2*(1 + eps*x*u) (:302)
+  switch (eq->eqn) {  // the functor's template arguments do not enter sigma_form
+    case DPAC_EQN_LQR: dpac::EqLQR<double, 1, 1>::sigma_form(*eq, td.sa, td.sb); break;
+    case DPAC_EQN_LQR_VAR: dpac::EqLQRVar<double, 1, 1>::sigma_form(*eq, td.sa, td.sb); break;
+    case DPAC_EQN_EKN: dpac::EqEKN<double, 1, 1>::sigma_form(*eq, td.sa, td.sb); break;
+    case DPAC_EQN_VDP: dpac::EqVDP<double, 2, 1>::sigma_form(*eq, td.sa, td.sb); break;
+    default: return fail(DPAC_EUNSUP, "no fused TD1 path for equation %d", eq->eqn);
+  }
+  td.p = eqn_lanes(eq->eqn, d);  // E::kP of the equation's k_td
   td.ldu = eq->control_dim;
   return 0;
 }

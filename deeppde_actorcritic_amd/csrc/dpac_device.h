@@ -45,6 +45,12 @@ __host__ __device__ constexpr int lanes_for_dim(int D) {
 __host__ __device__ constexpr int comps_per_lane(int D) {
   return (D + lanes_for_dim(D) - 1) / lanes_for_dim(D);
 }
+// The lane split of each equation family's kernels (the TUs dpac_eqn_*.hip instantiate the
+// functors with it; the fused TD1 row kernels must use the same one).  VDP's cyclic coupling
+// keeps a trajectory in one lane.
+__host__ __device__ constexpr int eqn_lanes(int eqn, int D) {
+  return eqn == DPAC_EQN_VDP ? 1 : lanes_for_dim(D);
+}
 
 // Ownership of one lane: the CONTIGUOUS components j = p*M + m (m < M), so a
 // lane moves one M-element vector per row and a group's lanes cover the row
@@ -443,6 +449,8 @@ struct EqLQR {
 #pragma unroll
     for (int m = 0; m < M; ++m) s[m] = sqrt2;
   }
+  // sigma() as sa * (1 + sb * x_j * u_j) for the fused TD1 row kernels (host side)
+  static void sigma_form(const dpac_eqn_params&, double& sa, double& sb) { sa = 1.4142135623730951; sb = 0.0; }
   __device__ __forceinline__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
     T a = 0;
 #pragma unroll
@@ -510,6 +518,10 @@ struct EqLQRVar {
 #pragma unroll
     for (int m = 0; m < M; ++m) s[m] = sqrt2 * (1 + (eps * x[m]) * u[m]);
   }
+  static void sigma_form(const dpac_eqn_params& e, double& sa, double& sb) {
+    sa = 1.4142135623730951;  // sqrt2 * (1 + eps * x * u) (equation.py:305)
+    sb = e.epsilon;
+  }
   __device__ __forceinline__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
     T a = 0;
 #pragma unroll
@@ -576,6 +588,7 @@ struct EqEKN {
 #pragma unroll
     for (int m = 0; m < M; ++m) s[m] = sqrt2;
   }
+  static void sigma_form(const dpac_eqn_params&, double& sa, double& sb) { sa = 1.4142135623730951; sb = 0.0; }
   __device__ __forceinline__ T w_part(const T (&x)[M], const T (&u)[MC]) const { return 0; }
   __device__ __forceinline__ T w_finish(T) const { return 1; }  // 0*sum(x) + 1 (:250)
   __device__ __forceinline__ T V_true(const T (&x)[M], T S, T r) const { return a3 * (r * r * r) - a2 * (r * r); }
@@ -653,6 +666,7 @@ struct EqVDP {
 #pragma unroll
     for (int m = 0; m < M; ++m) s[m] = sqrt2;
   }
+  static void sigma_form(const dpac_eqn_params&, double& sa, double& sb) { sa = 1.4142135623730951; sb = 0.0; }
   __device__ __forceinline__ T w_part(const T (&x)[M], const T (&u)[MC]) const {
     T dv1[C], dv2[C];
     Lop(x, dv1);

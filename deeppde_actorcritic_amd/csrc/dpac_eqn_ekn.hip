@@ -4,7 +4,7 @@
 
 namespace dpac {
 template <typename T, int D>
-using EqEKNFor = EqEKN<T, D, lanes_for_dim(D)>;
+using EqEKNFor = EqEKN<T, D, eqn_lanes(DPAC_EQN_EKN, D)>;
 using eknDims = DimList<EqEKNFor, DPAC_DIMS>;
 #if DPAC_TU_DOUBLE
 int dispatch_ekn_f64(const OpArgs& a) { return eknDims::dispatch<double>(a); }

@@ -4,7 +4,7 @@
 
 namespace dpac {
 template <typename T, int D>
-using EqLQRFor = EqLQR<T, D, lanes_for_dim(D)>;
+using EqLQRFor = EqLQR<T, D, eqn_lanes(DPAC_EQN_LQR, D)>;
 using lqrDims = DimList<EqLQRFor, DPAC_DIMS>;
 #if DPAC_TU_DOUBLE
 int dispatch_lqr_f64(const OpArgs& a) { return lqrDims::dispatch<double>(a); }

@@ -4,7 +4,7 @@
 
 namespace dpac {
 template <typename T, int D>
-using EqLQRVarFor = EqLQRVar<T, D, lanes_for_dim(D)>;
+using EqLQRVarFor = EqLQRVar<T, D, eqn_lanes(DPAC_EQN_LQR_VAR, D)>;
 using lqrvarDims = DimList<EqLQRVarFor, DPAC_DIMS>;
 #if DPAC_TU_DOUBLE
 int dispatch_lqrvar_f64(const OpArgs& a) { return lqrvarDims::dispatch<double>(a); }

@@ -4,7 +4,7 @@
 
 namespace dpac {
 template <typename T, int D>
-using EqVDPFor = EqVDP<T, D, 1>;
+using EqVDPFor = EqVDP<T, D, eqn_lanes(DPAC_EQN_VDP, D)>;
 using vdpDims = DimList<EqVDPFor, DPAC_DIMS_EVEN>;
 #if DPAC_TU_DOUBLE
 int dispatch_vdp_f64(const OpArgs& a) { return vdpDims::dispatch<double>(a); }

@@ -221,9 +221,14 @@ def rollout_nn(eqp, scheme: int, x0: torch.Tensor, dw: torch.Tensor, total_time:
     if save:
         saves = (torch.empty(N, B, sum(mlp.widths[1:]), **kw),
                  torch.empty(N, B, dtype=torch.int32, device=x0.device), torch.empty(N, B, **kw))
-        mb = _lib.load().dpac_rollout_nn_mask_tile_bytes(ctypes.byref(mlp.struct))
-        if MASK_BPTT and x0.dtype == torch.float32 and mb > 0:
-            mask = torch.empty(N, (B + 15) // 16, mb, dtype=torch.uint8, device=x0.device)
+        if MASK_BPTT:  # only where the kernel will write one (16-row fast path)
+            lib = _lib.load()
+            nb = lib.dpac_rollout_nn_mask_bytes(ctypes.byref(mlp.struct), _dtype_id(x0), B, N)
+            if nb < 0:
+                raise _lib.DpacError("dpac_rollout_nn_mask_bytes", int(nb), lib.dpac_last_error().decode())
+            if nb > 0:
+                mb = lib.dpac_rollout_nn_mask_tile_bytes(ctypes.byref(mlp.struct))
+                mask = torch.empty(N, (B + 15) // 16, mb, dtype=torch.uint8, device=x0.device)
     call("dpac_rollout_nn_fwd_masked", ctypes.byref(eqp), scheme, _dtype_id(x0), B, N, float(total_time),
          ctypes.byref(mlp.struct), _ptr(x0.contiguous()), _ptr(dw.contiguous()), _ptr(x), _ptr(dt),
          _ptr(coef), _ptr(u), _lib.COST_CRITIC if cost_order is None else cost_order, _ptr(y),

@@ -70,9 +70,15 @@ class DataParallel:
         for t in tensors:
             dist.broadcast(t.data, src=src, group=self.group)
 
-    def broadcast_int(self, value: int, src: int = 0) -> int:
-        """Rank src's integer on every rank (e.g. a seed drawn on rank 0)."""
-        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
+    def broadcast_int(self, value: int, src: int = 0, device=None) -> int:
+        """Rank src's integer on every rank (e.g. a seed drawn on rank 0).  Under nccl the
+        tensor lives on `device` (the caller's GPU; RCCL needs each rank on its own card)."""
+        if dist.get_backend(self.group) == "nccl":
+            dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+            if dev.type != "cuda":
+                raise ValueError(f"broadcast_int over nccl needs a GPU device, got {dev}")
+        else:
+            dev = torch.device("cpu")
         t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
         dist.broadcast(t, src=src, group=self.group)
         return int(t.item())
@@ -113,7 +119,7 @@ class SingleProcess:
     def broadcast_(self, tensors, src=0):
         pass
 
-    def broadcast_int(self, value, src=0):
+    def broadcast_int(self, value, src=0, device=None):
         return int(value)
 
     def gather_rows(self, t, total):

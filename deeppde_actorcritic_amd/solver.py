@@ -443,7 +443,8 @@ class ActorCriticSolver(object):
         self.par = parallel or SingleProcess()
         # one seed for every rank: the Philox stream is keyed by global trajectory index,
         # so the shards of a batch are its rows whatever the world size
-        self.seed = self.par.broadcast_int(seed if seed is not None else np.random.randint(0, 2 ** 31 - 1))
+        self.seed = self.par.broadcast_int(seed if seed is not None else np.random.randint(0, 2 ** 31 - 1),
+                                          device=self.device)
         self.sampler = sampler or self.train_config.get("sampler", "device")
         if self.sampler not in ("device", "host"):
             raise ValueError("sampler must be 'device' or 'host'")

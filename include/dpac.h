@@ -49,7 +49,9 @@
 extern "C" {
 #endif
 
-#define DPAC_ABI_VERSION 1
+/* 2: dpac_rollout_nn_bwd / dpac_mlp_rows_bwd take weight_t_km (round 2); adds
+ * dpac_rollout_nn_mask_bytes.  Bindings must refuse a library of another version. */
+#define DPAC_ABI_VERSION 2
 
 /* status codes besides hipError_t values */
 #define DPAC_OK 0
@@ -305,6 +307,12 @@ int dpac_rollout_nn_bwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype
  * DPAC_NN_TILE=16): *mask_written (host) reports whether it was; pass it to the backward only
  * then.  Results are bitwise those of the unmasked pair. */
 int32_t dpac_rollout_nn_mask_tile_bytes(const dpac_mlp* actor);
+/* The save_mask bytes dpac_rollout_nn_fwd_masked writes for this call
+ * (N * ceil(B / 16) * dpac_rollout_nn_mask_tile_bytes), or 0 where it writes none (float64,
+ * 4-row tiles at B <= 1024, no fast path): allocate the mask only when this is > 0.
+ * -1 on a bad argument. */
+int64_t dpac_rollout_nn_mask_bytes(const dpac_mlp* actor, int32_t dtype, int64_t num_sample,
+                                   int32_t num_steps);
 int dpac_rollout_nn_fwd_masked(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
                                int64_t num_sample, int32_t num_steps, double total_time,
                                const dpac_mlp* actor, const void* x0, const void* dw, void* x,

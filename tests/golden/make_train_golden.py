@@ -5,7 +5,7 @@ CPU oracle (test infrastructure; run in the build container, not on the GPU box)
     python tests/golden/make_train_golden.py [--threads 8]
 
 -> tests/golden/train_lqr_d20_B4096.npz: solver.py:36-71 run verbatim by the oracle for
-3 iterations (logging every iteration) on BASELINE configs[1] (lqr_d20: d = c = 20,
+6 iterations (logging every iteration) on BASELINE configs[1] (lqr_d20: d = c = 20,
 N = 100, T = 0.2, 3x200 MLPs, TD1, adaptive, normal sampling, actor-critic) with
 batch_size 4096 and valid_size 512, initial weights from the product's initialiser
 (seed 11: the Keras initialisers drawn from torch.Generator().manual_seed(11) in the
@@ -30,7 +30,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
-SEED_PARAMS, SEED_NUMPY, ITERS, BATCH, VALID = 11, 123, 3, 4096, 512
+SEED_PARAMS, SEED_NUMPY, ITERS, BATCH, VALID = 11, 123, 6, 4096, 512
 
 
 def config():

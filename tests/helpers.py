@@ -14,6 +14,23 @@ EQN_COEFFS = {  # per-equation eqn_config keys, values of the shipped configs
 }
 
 
+# the reference's configs/lqr_d5.json, restated verbatim (the reference tree does not travel to
+# the GPU box): BASELINE configs[0] is this file with TD2, the naive scheme and batch 256
+SHIPPED_LQR_D5 = {
+    "eqn_config": {"_comment": "linear quadratic regulator", "eqn_name": "LQR",
+                   "total_time_critic": 0.2, "total_time_actor": 0.2, "dim": 5, "control_dim": 5,
+                   "num_time_interval_critic": 50, "num_time_interval_actor": 50, "discount": 1.0,
+                   "p": 1.0, "q": 1.0, "beta": 1.0, "R": 1.0},
+    "net_config": {"num_hiddens_critic": [200, 200], "num_hiddens_actor": [200, 200],
+                   "lr_values_critic": [1e-3, 1e-4, 1e-5], "lr_boundaries_critic": [20000, 30000],
+                   "lr_values_actor": [1e-3, 1e-4, 1e-5], "lr_boundaries_actor": [20000, 30000],
+                   "num_iterations": 40000, "batch_size": 1024, "valid_size": 1024,
+                   "logging_frequency": 100, "dtype": "float64", "verbose": True},
+    "train_config": {"sample_type": "normal", "scheme": "adaptive", "TD_type": "TD1",
+                     "train": "actor-critic"},
+}
+
+
 def eqn_config(name, dim, control_dim=None, T=0.2, N=10, discount=None, R=1.0):
     if control_dim is None:
         control_dim = dim // 2 if name == "VDP" else dim

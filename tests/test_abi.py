@@ -148,3 +148,77 @@ def test_unsupported_dim_is_eunsup():
     with pytest.raises(_lib.DpacError) as ei:
         _lib.call("dpac_flag_init", ctypes.byref(p), 1, 0, 16, 10, 0.2, d, d, None)
     assert ei.value.code == _lib.DPAC_EUNSUP
+
+
+def test_fused_td1_rejects_eikonal_head():
+    """The fused TD1 G network (dpac_mlp_rows_fwd_td1 / _bwd_td1) refuses an Eikonal head at the
+    C boundary, not only in the solver (_critic_split_ok)."""
+    p = _params(_lib.EQN_EKN, 20, 20)
+    p.a2, p.a3 = 1.2, 0.2
+    d = ctypes.c_void_p(0x1000)
+    net = _net(20, 20)
+    net.ekn_head = 1
+    with pytest.raises(_lib.DpacError) as ei:
+        _lib.call("dpac_mlp_rows_fwd_td1", ctypes.byref(p), 0, 64, ctypes.byref(net), d, 20, d, d, d,
+                  None, None)
+    assert ei.value.code == _lib.DPAC_EINVAL and "eikonal" in str(ei.value).lower()
+    with pytest.raises(_lib.DpacError) as ei:
+        _lib.call("dpac_mlp_rows_bwd_td1", ctypes.byref(p), 0, 64, ctypes.byref(net), (ctypes.c_void_p * 2)(d, d),
+                  None, d, d, 20, d, d, d, d, None, None)
+    assert ei.value.code == _lib.DPAC_EINVAL
+
+
+def _actor_shape_net(L=3, d=20, h=200, km=True):
+    """A dpac_mlp with the actor shape of the shipped configs (dummy pointers)."""
+    n = _lib.Mlp()
+    n.n_hidden = L
+    n.width[0] = d
+    for i in range(1, L + 1):
+        n.width[i] = h
+    n.width[L + 1] = d
+    for i in range(L + 2):
+        n.bn_scale[i] = n.bn_shift[i] = 0x1000
+    for i in range(L + 1):
+        n.weight[i] = 0x1000
+        n.weight_km[i] = 0x1000 if km else None
+    n.bias = 0x1000
+    return n
+
+
+def test_mask_bytes_query(monkeypatch):
+    """dpac_rollout_nn_mask_bytes mirrors the forward's kernel choice: a mask only for float
+    16-row tiles (B > 1024 or DPAC_NN_TILE=16) on the actor-shape fast path."""
+    lib = _lib.load()
+    monkeypatch.delenv("DPAC_NN_TILE", raising=False)
+    monkeypatch.delenv("DPAC_NN_FAST", raising=False)
+    q = lambda net, dt, B, N: lib.dpac_rollout_nn_mask_bytes(ctypes.byref(net), dt, B, N)
+    net = _actor_shape_net()
+    tile = lib.dpac_rollout_nn_mask_tile_bytes(ctypes.byref(net))
+    assert tile == 13 * 64 * 3
+    assert q(net, _lib.F32, 2048, 100) == 100 * 128 * tile
+    assert q(net, _lib.F32, 1030, 7) == 7 * 65 * tile
+    assert q(net, _lib.F32, 1024, 100) == 0          # 4-row tiles
+    assert q(net, _lib.F64, 4096, 100) == 0          # float only
+    assert q(_actor_shape_net(km=False), _lib.F32, 4096, 100) == 0  # no k-major images
+    assert q(_actor_shape_net(h=64), _lib.F32, 4096, 100) == 0      # not 13 column tiles
+    monkeypatch.setenv("DPAC_NN_TILE", "16")
+    assert q(net, _lib.F32, 100, 10) == 10 * 7 * tile
+    monkeypatch.setenv("DPAC_NN_FAST", "0")
+    assert q(net, _lib.F32, 4096, 10) == 0
+    assert q(net, _lib.F32, 0, 10) == -1 and q(net, 7, 16, 10) == -1
+
+
+def test_abi_version_mismatch_is_refused(tmp_path):
+    """_lib.load() refuses a library whose dpac_abi_version differs from the bindings' (a stale
+    build would take shifted arguments), before binding any entry point."""
+    import subprocess
+    import sys
+    src = tmp_path / "old.c"
+    src.write_text("int dpac_abi_version(void) { return 1; }\n")
+    so = tmp_path / "libold.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    code = ("from deeppde_actorcritic_amd import _lib\n"
+            "try:\n    _lib.load()\nexcept _lib.DpacUnavailable as e:\n    print('REFUSED', e)\n")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                         env=dict(os.environ, DPAC_LIB=str(so)))
+    assert "REFUSED" in out.stdout and "DPAC_ABI_VERSION 1" in out.stdout, out.stdout + out.stderr

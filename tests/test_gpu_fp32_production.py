@@ -1,0 +1,198 @@
+"""GPU: the float32 PRODUCTION path against the float64 oracle (north_star: "outputs must match
+the reference ... within a stated fp32 tolerance (value-function L2 error and control error)").
+
+The production float32 path differs from the float64 one in code, not only in precision:
+  * the actor-shape fast path of the fused rollout / BPTT (16-row MFMA tiles, narrow layers'
+    weights in VGPRs; taken for B > 1024 and 193..208-wide hidden layers);
+  * the BPTT reading the forward's activation sign bits (dpac_rollout_nn_*_masked);
+  * the k-major weight images (dwordx4 B loads);
+  * the critic's G network with the TD1 dot fused (dpac_mlp_rows_fwd_td1), HIP graphs and the
+    split critic / actor steps on side streams.
+Every test here runs that path (asserted where the path is observable) against the float64
+oracle (oracle/, the torch-CPU restatement of solver.py / equation.py) on the same inputs and
+initial weights.
+
+Tolerances (float32 against float64):
+  * rollout: <= 1e-3 of trajectories may flip an exit decision (|x| = R is a discontinuity);
+    matched trajectories within 1e-5 (1 + |ref|) on x, u and dt;
+  * gradients (flipped trajectories removed from both sides): per tensor
+    max |g - g_ref| <= 1e-3 * max |g_ref|;
+  * training, lqr_d20 at BASELINE's B = 4096 (6 iterations, validated after every one, against
+    tests/golden/train_lqr_d20_B4096.npz): |err_value - ref| <= 1e-5 and
+    |err_control - ref| <= 1e-5 (absolute, relative-L2 units) at every logged step, the
+    losses within 1e-4 relative, and every parameter summary within 2e-4 (1 + |ref|).
+Measured on MI355X (round 3): paths 6.3e-7, gradients 9.6e-5 (critic) / 1.2e-6 (actor),
+err_value 9.1e-7, err_control 4.5e-7, parameters 2.1e-5 (profiles/r03_fp32_parity.txt).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from deeppde_actorcritic_amd import _lib, ops
+from deeppde_actorcritic_amd import equation as peq
+from deeppde_actorcritic_amd import solver as psol
+from deeppde_actorcritic_amd.config import baseline_config, set_floatx
+from oracle import equations as oeq
+from oracle import solver as osol
+from tests.helpers import full_config, rel_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_lqr_d20_B4096.npz")
+
+TOL_FLIP = 1e-3      # fraction of trajectories allowed to flip an exit decision
+TOL_PATH = 1e-5      # matched trajectories, |a - b| <= TOL_PATH (1 + |b|)
+TOL_GRAD = 1e-3      # per tensor, max |g - g_ref| <= TOL_GRAD max |g_ref|
+TOL_ERR = 1e-5       # err_value / err_control, absolute, every logged step
+TOL_LOSS = 1e-4      # validation losses, |a - b| <= TOL_LOSS (1 + |b|)
+TOL_PARAM = 2e-4     # parameter summaries, |a - b| <= TOL_PARAM (1 + |b|)
+
+
+@pytest.fixture(autouse=True)
+def _default_paths(monkeypatch):
+    """The production selection: no test override of the kernel choice."""
+    for k in ("DPAC_NN_TILE", "DPAC_NN_FAST", "DPAC_BPTT", "DPAC_MASK_BPTT", "DPAC_WEIGHT_KM"):
+        monkeypatch.delenv(k, raising=False)
+    assert ops.MASK_BPTT and ops.WEIGHT_KM == "on" and ops.CRITIC_TD1 == "fused"
+    assert ops.BPTT_MODE == "fused" and ops.ROW_MLP == "kernel" and ops.PARAM_GRADS == "kernel"
+    yield
+    set_floatx("float64")
+
+
+def _pair(cfg, seed):
+    bp = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
+    sp = psol.ActorCriticSolver(cfg, bp, seed=seed, sampler="host", graphs=False)
+    params = {"critic": sp.model_critic.NN_value.export_params(),
+              "critic_grad": sp.model_critic.NN_value_grad.export_params(),
+              "actor": sp.model_actor.NN_control.export_params()}
+    return sp, osol.ActorCriticSolver(cfg, oeq.make(cfg.eqn_config), params=params)
+
+
+def _f32(a):
+    return torch.as_tensor(np.asarray(a), dtype=torch.float32, device=DEV)
+
+
+@pytest.mark.parametrize("name,B", [("LQR", 1040), ("LQR", 2050), ("EKN", 1100), ("VDP", 1043),
+                                    ("LQR_var", 1060)])
+def test_fp32_sixteen_row_fast_path_forward_vs_oracle(name, B):
+    """The float rollout with the actor MLP at B > 1024 (16-row tiles, actor-shape fast path,
+    sign-bit mask written) against the oracle's propagate_adaptive with the oracle DeepNN."""
+    N, T = 50, 0.2
+    cfg = full_config(name, 20, N=N, hidden=(200, 200, 200), scheme="adaptive", dtype="float32")
+    sp, so = _pair(cfg, 21)
+    net = sp.model_actor.NN_control
+    eo = so.bsde
+    np.random.seed(31)
+    x0, dw, _ = eo.sample_normal(B, N)
+    xr, dtr, cr = eo.propagate_adaptive(B, x0, dw, so.model_actor.NN_control, False, T, N, False)
+    x, dt, coef, u, _, _, saves = ops.rollout_nn(
+        sp.bsde.params(), _lib.SCHEME_ADAPTIVE, _f32(x0), _f32(dw).permute(2, 0, 1).contiguous(), T, N,
+        net.mlp_view(), cost_order=_lib.COST_ACTOR, save=True)
+    assert saves[3] is not None, "the 16-row fast path did not run (no sign-bit mask written)"
+    same = np.all(coef.cpu().numpy() == cr.numpy(), axis=1)
+    flips = float(np.mean(~same))
+    print(f"\n[fp32 fwd {name} B={B}] flip fraction {flips:.2e}")
+    assert flips <= TOL_FLIP
+    xm = x.permute(1, 2, 0).cpu().double().numpy()[same]
+    err = np.max(np.abs(xm - xr.numpy()[same]) / (1 + np.abs(xr.numpy()[same])))
+    print(f"[fp32 fwd {name} B={B}] matched max rel |dx| {err:.2e}")
+    assert err <= TOL_PATH
+    assert rel_close(dt.cpu().double().numpy()[same], dtr.numpy()[same], TOL_PATH)
+    with torch.no_grad():
+        ur = torch.stack([so.model_actor.NN_control(xr[:, :, t]) for t in range(N)])  # [N, B, c]
+    assert rel_close(u.cpu().double().numpy()[:, same], ur.numpy()[:, same], TOL_PATH)
+
+
+def _matched(sp, so, data, N, T):
+    """Trajectories whose float32 production rollout keeps every exit decision of the oracle."""
+    x0, dw, _ = data
+    _, _, cr = so.bsde.propagate_adaptive(x0.shape[0], x0, dw, so.model_actor.NN_control, False, T, N, False)
+    _, _, coef, _, _, _, _ = ops.rollout_nn(
+        sp.bsde.params(), _lib.SCHEME_ADAPTIVE, _f32(x0), _f32(dw).permute(2, 0, 1).contiguous(), T, N,
+        sp.model_actor.NN_control.mlp_view(), want_u=False)
+    return np.all(coef.cpu().numpy() == cr.numpy(), axis=1)
+
+
+def _grad_err(gp, go):
+    worst = 0.0
+    for a, b in zip(gp, go):
+        if b is None:
+            assert a is None or float(a.abs().max()) == 0.0
+            continue
+        a = a.detach().to("cpu", torch.float64)
+        scale = float(b.detach().abs().max())
+        worst = max(worst, float((a - b.detach()).abs().max()) / max(scale, 1e-30))
+    return worst
+
+
+@pytest.mark.parametrize("name,B", [("LQR", 1100), ("LQR_var", 1100), ("EKN", 1040)])
+def test_fp32_production_gradients_vs_oracle_tape(name, B):
+    """The critic's and the actor's float32 gradients from the production kernels (critic_front +
+    critic_G_back: fused TD1 G network; actor_forward + actor_grads_from: 16-row fast path,
+    sign-bit-mask BPTT, k-major images, parameter-gradient kernel) against the oracle's
+    GradientTape restatement (float64) on the same batch."""
+    N, T = 50, 0.2
+    cfg = full_config(name, 20, N=N, hidden=(200, 200, 200), batch=B, scheme="adaptive", td="TD1",
+                      dtype="float32")
+    sp, so = _pair(cfg, 5)
+    np.random.seed(17)
+    dc = so.bsde.sample_normal(B, N)
+    da = so.bsde.sample_normal(B, N)
+    keep_c, keep_a = _matched(sp, so, dc, N, T), _matched(sp, so, da, N, T)
+    print(f"\n[fp32 grads {name}] flips critic {np.sum(~keep_c)} actor {np.sum(~keep_a)} of {B}")
+    assert np.mean(~keep_c) <= TOL_FLIP and np.mean(~keep_a) <= TOL_FLIP
+    dc = tuple(a[keep_c] for a in dc)
+    da = tuple(a[keep_a] for a in da)
+    assert min(dc[0].shape[0], da[0].shape[0]) > 1024  # still the 16-row fast path
+    # critic: the production split step, on one batch
+    front = sp.critic_front(dc)
+    assert len(front) == 6, "the fused TD1 critic path did not run"
+    gp_c = front[0] + sp.critic_G_back(front)
+    go_c, _ = so.grad_critic(dc, False, False)
+    # actor: forward with saves (sign-bit mask) + BPTT kernels
+    fwd = sp.actor_forward(da)
+    assert fwd[3][6] is not None, "the actor forward wrote no sign-bit mask"
+    gp_a = sp.actor_grads_from(fwd)
+    go_a, _ = so.grad_actor(da, False, False, False)
+    ec, ea = _grad_err(gp_c, go_c), _grad_err(gp_a, go_a)
+    print(f"[fp32 grads {name}] critic max rel err {ec:.2e}, actor {ea:.2e}")
+    assert ec <= TOL_GRAD and ea <= TOL_GRAD
+
+
+def _summarize(tensors):
+    out = []
+    for t in tensors:
+        t = t.detach().to("cpu", torch.float64).reshape(-1)
+        out.append([float(t.sum()), float((t * t).sum())] + t[:16].tolist() + [0.0] * (16 - min(16, t.numel())))
+    return np.array(out, dtype=np.float64)
+
+
+def test_fp32_production_training_lqr_d20_b4096_vs_oracle_vectors():
+    """BASELINE configs[1] (lqr_d20, TD1, normal sampling, adaptive, B = 4096, 3x200 MLPs)
+    trained in float32 on the production path — HIP graphs, the split critic step with the
+    fused TD1 G network, the actor step on the 16-row fast path with the sign-bit-mask BPTT —
+    from the oracle's initial weights and numpy sample stream, against the float64 oracle's
+    6 iterations (tests/golden/make_train_golden.py)."""
+    g = np.load(GOLDEN)
+    seed_params, seed_np, iters, batch, valid = (int(v) for v in g["meta"])
+    assert iters >= 5 and batch > 1024
+    cfg = baseline_config(iters, 1, "float32", batch, valid, "lqr_d20")
+    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=seed_params, sampler="host", graphs=True)
+    np.random.seed(seed_np)
+    hist = sp.train()[0]
+    assert sp._actor_split_ok() and sp._critic_split_ok()
+    assert {k[0] for k in sp._graphs} == {"actor_split", "critic_split"}
+    ref = g["history"]
+    assert hist.shape == ref.shape
+    d_val = np.abs(hist[:-1, 3] - ref[:-1, 3])
+    d_ctl = np.abs(hist[:-1, 5] - ref[:-1, 5])
+    d_loss = np.abs(hist[:, 1:3] - ref[:, 1:3]) / (1 + np.abs(ref[:, 1:3]))
+    got = _summarize(sp.critic_variables() + sp.actor_variables())
+    d_par = np.abs(got - g["params"]) / (1 + np.abs(g["params"]))
+    print(f"\n[fp32 training lqr_d20 B={batch}] max |d err_value| {d_val.max():.2e}, "
+          f"max |d err_control| {d_ctl.max():.2e}, losses {d_loss.max():.2e}, params {d_par.max():.2e}")
+    assert d_val.max() <= TOL_ERR and d_ctl.max() <= TOL_ERR
+    assert d_loss.max() <= TOL_LOSS
+    assert got.shape == g["params"].shape and d_par.max() <= TOL_PARAM

@@ -75,3 +75,70 @@ def test_lqr_d20_baseline_batch_matches_oracle_vectors(graphs):
     got = summarize(sp.critic_variables() + sp.actor_variables())
     assert got.shape == g["params"].shape
     assert rel_close(got, g["params"], 1e-8)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+@pytest.mark.parametrize("name,d", [("LQR", 20), ("VDP", 4)])
+def test_bounded_sampling_training_matches_oracle(name, d, graphs):
+    """sample_type "bounded" (solver.py:26-27 -> equation.py:25-36: the 3-point increments
+    +-sqrt(3) w.p. 1/6, 0 w.p. 2/3) end to end: the reference's numpy stream of
+    sample_bounded feeds both sides; 3 iterations, logged after each, 1e-8 (float64)."""
+    cfg = full_config(name, d, N=10, hidden=(32, 32), batch=48, valid=48, iters=3, log_freq=1,
+                      train="actor-critic", td="TD1", sample="bounded")
+    sp, so = pair(cfg, 19, graphs)
+    np.random.seed(71)
+    hp = sp.train()
+    np.random.seed(71)
+    ho = so.train()
+    assert hp[0].shape == ho.shape == (5, 9)
+    assert rel_close(hp[0][:, 1:8], ho[:, 1:8], 1e-8)
+    for vp, vo in zip(sp.critic_variables() + sp.actor_variables(), so.critic_vars() + so.actor_vars()):
+        assert rel_close(vp.detach().cpu(), vo.detach(), 1e-8)
+
+
+def config0(dtype):
+    """BASELINE configs[0]: the reference's configs/lqr_d5.json with TD2, the naive scheme and
+    batch 256 (3 iterations, logged after each)."""
+    from deeppde_actorcritic_amd.config import munchify
+    from tests.helpers import SHIPPED_LQR_D5
+    import copy
+    c = copy.deepcopy(SHIPPED_LQR_D5)
+    c["train_config"].update(TD_type="TD2", scheme="naive")
+    c["net_config"].update(batch_size=256, num_iterations=3, logging_frequency=1, dtype=dtype,
+                           verbose=False)
+    return munchify(c)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_baseline_config0_lqr_d5_td2_naive_b256_matches_oracle(graphs):
+    """BASELINE configs[0] end to end (float64, the reference's dtype) against the live
+    oracle: shipped nets (2x200), N = 50, T = 0.2, valid_size 1024; 1e-8."""
+    cfg = config0("float64")
+    sp, so = pair(cfg, 23, graphs)
+    np.random.seed(29)
+    hp = sp.train()
+    np.random.seed(29)
+    ho = so.train()
+    assert hp[0].shape == ho.shape == (5, 9)
+    assert rel_close(hp[0][:, 1:8], ho[:, 1:8], 1e-8)
+    for vp, vo in zip(sp.critic_variables() + sp.actor_variables(), so.critic_vars() + so.actor_vars()):
+        assert rel_close(vp.detach().cpu(), vo.detach(), 1e-8)
+    assert sp.model_critic.td == 2  # TD2: G is never evaluated, its variables never move
+    g0 = sp.model_critic.NN_value_grad.export_params()
+    assert all(torch.equal(a, b) for a, b in zip(g0["W"], so.model_critic.NN_value_grad.params["W"]))
+
+
+def test_baseline_config0_float32_matches_oracle():
+    """configs[0] on the float32 production path (HIP graphs; B = 256 takes the 4-row MFMA
+    rollout kernel) against the float64 oracle: |d err_value|, |d err_control| <= 1e-5 at every
+    logged step (the fp32 tolerance of tests/test_gpu_fp32_production.py)."""
+    cfg = config0("float32")
+    sp, so = pair(cfg, 23, True)
+    np.random.seed(29)
+    hp = sp.train()[0]
+    np.random.seed(29)
+    ho = so.train()
+    dv, dc = np.abs(hp[:-1, 3] - ho[:-1, 3]).max(), np.abs(hp[:-1, 5] - ho[:-1, 5]).max()
+    print(f"\n[configs[0] fp32] max |d err_value| {dv:.2e}, |d err_control| {dc:.2e}")
+    assert dv <= 1e-5 and dc <= 1e-5
+    assert rel_close(hp[:, 1:3], ho[:, 1:3], 1e-4)

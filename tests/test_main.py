@@ -8,21 +8,11 @@ import pytest
 
 import main as dpac_main
 from deeppde_actorcritic_amd.config import load_config
+from tests.helpers import SHIPPED_LQR_D5
 
-# the reference's configs/lqr_d5.json layout, shrunk (iterations, batch) for a test run
-LQR_D5 = {
-    "eqn_config": {"_comment": "linear quadratic regulator", "eqn_name": "LQR",
-                   "total_time_critic": 0.1, "total_time_actor": 0.1, "dim": 5, "control_dim": 5,
-                   "num_time_interval_critic": 50, "num_time_interval_actor": 50, "discount": 1.0,
-                   "p": 1.0, "q": 1.0, "beta": 1.0, "R": 1.0},
-    "net_config": {"num_hiddens_critic": [200, 200], "num_hiddens_actor": [200, 200],
-                   "lr_values_critic": [1e-3, 1e-4, 1e-5], "lr_boundaries_critic": [30000, 40000],
-                   "lr_values_actor": [1e-3, 1e-4, 1e-5], "lr_boundaries_actor": [30000, 40000],
-                   "num_iterations": 40000, "batch_size": 256, "valid_size": 256,
-                   "logging_frequency": 10, "dtype": "float64", "verbose": True},
-    "train_config": {"sample_type": "normal", "scheme": "adaptive", "TD_type": "TD1",
-                     "train": "actor-critic"},
-}
+# the reference's configs/lqr_d5.json verbatim; the test run overrides only num_iterations
+# (--num_iterations 200, logged at 0, 100, 200)
+LQR_D5 = SHIPPED_LQR_D5
 
 
 def write_config(tmp_path, cfg):
@@ -46,15 +36,15 @@ def test_main_writes_reference_logs(tmp_path, dtype):
     path = write_config(tmp_path, LQR_D5)
     logs = tmp_path / "logs"
     hist = dpac_main.main(["--config_path", path, "--exp_name", "lqr_d5", "--log_dir", str(logs),
-                           "--num_iterations", "20", "--dtype", dtype, "--seed", "3"])
+                           "--num_iterations", "200", "--dtype", dtype, "--seed", "3"])
     char = "normal_adaptive_TD1_actor-critic"
     files = sorted(os.listdir(logs))
     assert files == sorted(["lqr_d5_config.json", f"lqr_d5_{char}.csv", f"lqr_d5_{char}_hist.csv"])
     h = np.loadtxt(logs / f"lqr_d5_{char}.csv", delimiter=",", skiprows=1)
-    assert h.shape == (4, 9) and np.array_equal(h[:3, 0], [0, 10, 20])  # 3 logs + true-loss row
+    assert h.shape == (4, 9) and np.array_equal(h[:3, 0], [0, 100, 200])  # 3 logs + true-loss row
     assert np.all(np.isfinite(h)) and h[2, 3] < h[0, 3]  # err_value decreases from init
     f = np.loadtxt(logs / f"lqr_d5_{char}_hist.csv", delimiter=",", skiprows=1)
-    assert f.shape == (256, 5 + 1 + 1 + 5 + 5)
+    assert f.shape == (1024, 5 + 1 + 1 + 5 + 5)  # valid_size rows
     assert np.allclose(hist[:, 1:8], h[:, 1:8], rtol=1e-5, atol=1e-12)  # CSV keeps 6 digits (%.5e)
     saved = json.loads((logs / "lqr_d5_config.json").read_text())
-    assert saved["net_config"]["num_iterations"] == 20 and saved["eqn_config"] == LQR_D5["eqn_config"]
+    assert saved["net_config"]["num_iterations"] == 200 and saved["eqn_config"] == LQR_D5["eqn_config"]
