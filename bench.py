@@ -77,6 +77,20 @@ def time_launches(launch, steps, warmup, world):
     return wall, per_launch_ms
 
 
+def time_launches_bracketed(launch, steps):
+    """Each of `steps` launches between its own HIP event pair (after the timed region, on
+    the same stream): the mean per-kernel duration without the dispatch gaps, the figure
+    rocprofv3's kernel trace reports (tools/rocprof_headline.py compares the two)."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(evs):
+        a.record()
+        launch(i)
+        b.record()
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+
 def max_over_ranks(v, world):
     if world == 1:
         return v
@@ -149,12 +163,28 @@ def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total
     torch.cuda.synchronize()
     barrier(world)
     ms = max_over_ranks(time.perf_counter() - t0, world) / iters * 1e3
-    # MLP work per iteration: critic ≈ 5, actor ≈ 6 MLP-forward equivalents
-    # per trajectory-step; reported as an achieved rate, not a roofline claim
+    # MLP work per iteration, in forward-pass equivalents (176 kFLOP per row at d = 20) per
+    # trajectory-step: EXECUTED by this build = 7 (actor forward in the critic's rollout, G
+    # forward, G backward chain + G parameter gradients = 2, actor forward with saves,
+    # BPTT chain, actor parameter gradients); the reference executes 11 (SURVEY §8(d),
+    # with its duplicated NN_control evaluations, quirk 7).  An achieved rate, not a roofline.
+    rate = Bg * N / (ms * 1e-3) * MLP_FLOP_PER_ROW / 1e12
     return {"config": name, "global_batch": Bg, "batch_per_gpu": Bg // max(world, 1), "horizon": N,
             "mlp": "20-200-200-200-%d" % cfg.eqn_config.control_dim, "ms_per_iteration": ms,
             "traj_steps_per_s": 2 * Bg * N / (ms * 1e-3),
-            "mlp_equiv_TFLOPs": 11 * MLP_FLOP_PER_ROW * Bg * N / (ms * 1e-3) / 1e12}
+            "mlp_executed_TFLOPs": 7 * rate, "mlp_reference_equiv_TFLOPs": 11 * rate,
+            "mlp_math": ops_mlp_math(dtype)}
+
+
+def ops_mlp_math(dtype):
+    """How this build's MLP kernels multiply (deeppde_actorcritic_amd.ops.MLP_MATH)."""
+    from deeppde_actorcritic_amd import ops
+    if dtype != torch.float32:
+        return "f64 MFMA (v_mfma_f64_16x16x4_f64)"
+    if ops.MLP_MATH == "x3":
+        return ("f32 via split-fp16 MFMA in the row-parallel critic kernels (3 v_mfma_f32_16x16x32_f16 "
+                "per product, f32 accumulate; f32-accurate, DESIGN.md 4.3), exact f32 MFMA elsewhere")
+    return "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
 
 
 def cpu_info():
@@ -218,7 +248,25 @@ def cpu_baseline(seconds=8.0):
             "value": 2 * Bt * 100 / el, "unit": "traj-steps/s", "ms_per_iteration": el * 1e3,
             "sample": f"1 oracle training iteration (critic + actor step) on lqr_d20, {tag}, B={Bt}, "
                       f"N=100, 3x200 MLPs ({el:.1f} s)"}
+    # the same rollout on ALL of the host's cores (f64), a bounded sample
     precision.set_dtype(torch.float64)
+    torch.set_num_threads(nproc)
+    eq = oeq.LQR(lqr_config())
+    np.random.seed(1234)
+    x0, dw, _ = eq.sample_normal(B_PER_GPU, HORIZON)
+    x0t, dwt = torch.as_tensor(x0), torch.as_tensor(dw)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        eq.propagate_adaptive(B_PER_GPU, x0t, dwt, None, False, T_TOTAL, HORIZON, True)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 50:
+            break
+    entries["rollout_f64_all_cores"] = {
+        "value": reps * B_PER_GPU * HORIZON / el, "unit": "traj-steps/s", "cores": nproc,
+        "sample": f"{reps} x oracle propagate_adaptive(cheat=True), f64, B={B_PER_GPU}, d={DIM}, N={HORIZON}, "
+                  f"torch threads = nproc = {nproc} ({el:.1f} s)"}
+    torch.set_num_threads(threads)
     head = entries["rollout_f64"]
     return {"value": head["value"], "unit": "traj-steps/s", "cores": threads, "kind": "port",
             "sample": head["sample"] + "; the reference's precision (float64, main.py:35)",
@@ -275,6 +323,8 @@ def main():
     wall, per_launch_ms = time_launches(rs.launcher(N_SETS), args.steps, args.warmup, world)
     wall = max_over_ranks(wall, world)
     per_launch_ms = max_over_ranks(per_launch_ms, world)
+    # the same cold launches, each between its own event pair (kernel time without gaps)
+    kernel_ms = max_over_ranks(time_launches_bracketed(rs.launcher(N_SETS), args.steps), world)
     ms_per_step = wall / args.steps * 1e3
     value = world * B * N * args.steps / wall
     algo_bytes = B * N * (2 * d + 2) * esize
@@ -293,7 +343,12 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": tsrc, "kernel": "dpac::k_rollout_staged",
-                     "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": per_launch_ms},
+                     "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": per_launch_ms,
+                     "avg_kernel_ms_bracketed": kernel_ms,
+                     "frac_bracketed": algo_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "note": "achieved/frac: one event pair over the K timed launches (per-launch time "
+                             "incl. dispatch gaps); *_bracketed: each launch between its own event pair, "
+                             "the per-kernel duration rocprofv3 reports (profiles/r03_rocprof_headline.json)"},
     }
     if not args.no_variants:
         variants = {}

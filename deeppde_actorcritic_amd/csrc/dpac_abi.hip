@@ -30,7 +30,7 @@ int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void
                         const void* save_z, const void* g_out, void* G, void* g_x, const TdRows* td,
                         hipStream_t s);
 int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
-                       void* wkm, void* wtkm, hipStream_t s);
+                       void* wkm, void* wtkm, void* wx3, void* wtx3, hipStream_t s);
 int adam_launch(int dtype, int n, const int64_t* numel, void* const* var, const void* const* grad,
                 void* const* m, void* const* v, double alpha, double b1, double b2, double eps,
                 hipStream_t s);
@@ -778,15 +778,18 @@ int dpac_equation_eval(const dpac_eqn_params* eq, int32_t what, int32_t dtype, i
 }
 
 int dpac_mlp_prepare(int32_t dtype, const dpac_mlp* net, double gamma_scale, void* scales,
-                     void* weight_t, void* weight_km, void* weight_t_km, void* stream) {
+                     void* weight_t, void* weight_km, void* weight_t_km, void* weight_x3,
+                     void* weight_t_x3, void* stream) {
   if (int e = check_net(net)) return e;
   if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
   DPAC_REQUIRE(scales);
-  if (weight_t || weight_km || weight_t_km)
+  if ((weight_x3 || weight_t_x3) && dtype != DPAC_F32)
+    return fail(DPAC_EINVAL, "split-fp16 images (weight_x3 / weight_t_x3) are float-only");
+  if (weight_t || weight_km || weight_t_km || weight_x3 || weight_t_x3)
     for (int i = 0; i <= net->n_hidden; ++i)
       if (!net->weight[i]) return fail(DPAC_EINVAL, "weight[%d] is NULL", i);
   const int r = mlp_prepare_launch(dtype, *net, gamma_scale, scales, weight_t, weight_km,
-                                   weight_t_km, (hipStream_t)stream);
+                                   weight_t_km, weight_x3, weight_t_x3, (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();
 }

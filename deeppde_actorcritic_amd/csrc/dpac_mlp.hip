@@ -5,6 +5,7 @@
 
 #include "dpac_mlp_grad.h"
 #include "dpac_mlp_rows.h"
+#include "dpac_mlp_x3.h"
 
 namespace dpac {
 
@@ -200,9 +201,66 @@ void set_td(MrArgs<T>& a, const TdRows* td) {
   a.td_sb = (T)td->sb;
 }
 
+// The split-fp16 row kernels (dpac_mlp_x3.h) when every image of the direction is given.
+inline bool x3_all(const dpac_mlp& net, const void* const* img) {
+  for (int i = 0; i <= net.n_hidden; ++i)
+    if (!img[i]) return false;
+  return true;
+}
+
+X3Args x3_args(const dpac_mlp& net, int64_t rows, const void* const* img, const TdRows* td) {
+  X3Args a{};
+  const MrArgs<float> m = mr_args<float>(net, rows);
+  a.rows = rows;
+  a.L = m.L;
+  for (int i = 0; i <= a.L + 1; ++i) {
+    a.width[i] = m.width[i];
+    a.scale[i] = m.scale[i];
+    a.shift[i] = m.shift[i];
+    a.zoff[i] = m.zoff[i];
+    a.goff[i] = m.goff[i];
+  }
+  for (int i = 0; i <= a.L; ++i) a.wx3[i] = (const _Float16*)img[i];
+  a.bias = m.bias;
+  a.ztot = m.ztot;
+  a.gtot = m.gtot;
+  if (td) {
+    a.td_x = (const float*)td->x;
+    a.td_ldx = td->ldx;
+    a.td_u = (const float*)td->u;
+    a.td_ldu = td->ldu;
+    a.td_dw = (const float*)td->dw;
+    a.td_p = td->p;
+    a.td_sa = (float)td->sa;
+    a.td_sb = (float)td->sb;
+  }
+  return a;
+}
+
+template <class K>
+int x3_launch(K kfn, const X3Args& a, hipStream_t s) {
+  if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kX3LdsBytes))
+    return (int)e;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)((a.rows + kX3Rows - 1) / kX3Rows)), dim3(kX3Threads), kX3LdsBytes, s,
+                     a);
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void* out,
              void* save_z, const TdRows* td, hipStream_t s) {
+  if constexpr (std::is_same<T, float>::value) {
+    if (x3_all(net, net.weight_x3)) {
+      X3Args a = x3_args(net, rows, net.weight_x3, td);
+      if (td) a.gdot = (float*)td->gdot;
+      a.x = (const float*)x;
+      a.ldx = ldx;
+      a.out = (float*)out;
+      a.z = (float*)save_z;
+      return x3_launch(k_mlp_rows_fwd_x3, a, s);
+    }
+  }
   MrArgs<T> a = mr_args<T>(net, rows);
   set_td(a, td);
   if (td) a.gdot = (T*)td->gdot;
@@ -219,6 +277,17 @@ int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void
 template <typename T>
 int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const void* save_z,
              const void* g_out, void* G, void* g_x, const TdRows* td, hipStream_t s) {
+  if constexpr (std::is_same<T, float>::value) {
+    if (x3_all(net, net.weight_t_x3)) {
+      X3Args a = x3_args(net, rows, net.weight_t_x3, td);
+      if (td) a.g_gdot = (const float*)td->g_gdot;
+      a.z = (float*)save_z;
+      a.g_out = (const float*)g_out;
+      a.G = (float*)G;
+      a.g_x = (float*)g_x;
+      return x3_launch(k_mlp_rows_bwd_x3, a, s);
+    }
+  }
   MrArgs<T> a = mr_args<T>(net, rows);
   set_td(a, td);
   if (td) a.g_gdot = (const T*)td->g_gdot;
@@ -261,3 +330,11 @@ int mlp_param_grads_launch(int dtype, int64_t rows, const dpac_mlp& net, double 
 }
 
 }  // namespace dpac
+
+#if DPAC_X3_TRACE
+// Timing builds only: copy the x3 row kernels' clock table (dpac_mlp_x3.h) to the host.
+extern "C" int dpac_debug_x3_trace(void* host, int64_t bytes) {
+  const int64_t n = bytes < (int64_t)sizeof(dpac::g_x3_trace) ? bytes : (int64_t)sizeof(dpac::g_x3_trace);
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(dpac::g_x3_trace), (size_t)n, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -86,6 +86,7 @@ int launch(int n, const int64_t* numel, void* const* var, const void* const* gra
 }
 
 // dpac_mlp_prepare: s_i = gamma_scale * gamma_i for every BN layer (concatenated)
+// (and the split-fp16 images x3_i / tx3_i of km_i / tkm_i's operands, float only)
 // and, optionally, for every dense layer (each segment concatenated over i):
 //   wt_i  = (W_i ⊙ s_{i+1})^T         [w_{i+1}][w_i]
 //   km_i  = W_i^T, k-major padded      [w_{i+1}][K16(w_i)]      (forward image)
@@ -103,11 +104,22 @@ struct PrepArgs {
   int64_t woff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets of wt_i in `wt`
   int64_t koff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets of km_i in `km`
   int64_t toff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets of tkm_i in `tkm`
+  int64_t xoff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets (halves) of x3_i in `x3`
+  int64_t yoff[DPAC_MLP_MAX_HIDDEN + 2];  // offsets (halves) of tx3_i in `tx3`
   T gscale;
   T *scales, *wt, *km, *tkm;
+  _Float16 *x3, *tx3;                     // split-fp16 images (float only)
 };
 
 __device__ __forceinline__ int k16(int k) { return (k + 15) / 16 * 16; }
+
+// element h (0..63) of chunk c of a split-fp16 column (dpac.h dpac_mlp.weight_x3): the hi
+// (h < 32) or lo half of operand value v at k = 32c + (h & 31); hi = fp16(v),
+// lo = fp16((v - hi) * 2^12), as dpac_mlp_x3.h splits activations.
+__device__ __forceinline__ _Float16 x3_part(float v, int h) {
+  const _Float16 hi = (_Float16)v;
+  return h < 32 ? hi : (_Float16)((v - (float)hi) * 4096.f);
+}
 
 template <typename T>
 __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> a) {
@@ -115,8 +127,28 @@ __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> 
   const int64_t nw = a.wt ? a.woff[a.L + 1] : 0;
   const int64_t nk = a.km ? a.koff[a.L + 1] : 0;
   const int64_t nt = a.tkm ? a.toff[a.L + 1] : 0;
-  for (int64_t e = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; e < ns + nw + nk + nt;
+  const int64_t nx = a.x3 ? a.xoff[a.L + 1] : 0;
+  const int64_t ny = a.tx3 ? a.yoff[a.L + 1] : 0;
+  const int64_t n4 = ns + nw + nk + nt;
+  for (int64_t e = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; e < n4 + nx + ny;
        e += (int64_t)gridDim.x * kAdamThreads) {
+    if (e >= n4) {  // split-fp16 images: [cols][ceil(K/32)][64] halves per layer
+      const bool fwd = e < n4 + nx;
+      const int64_t f = fwd ? e - n4 : e - n4 - nx;
+      const int64_t* off = fwd ? a.xoff : a.yoff;
+      int i = 0;
+      while (f >= off[i + 1]) ++i;
+      const int64_t r = f - off[i];
+      const int K = fwd ? a.width[i] : a.width[i + 1], nch = (K + 31) / 32;
+      const int64_t n = r / (64 * nch), c = (r / 64) % nch;
+      const int h = (int)(r % 64), k = 32 * (int)c + (h & 31);
+      float v = 0.f;
+      if (k < K)  // forward: W_i[k][n]; backward: W_i[n][k] * s_{i+1}[k] (as tkm_i)
+        v = fwd ? (float)a.W[i][(int64_t)k * a.width[i + 1] + n]
+                : (float)(a.W[i][n * K + k] * (a.gscale * a.gamma[i + 1][k]));
+      (fwd ? a.x3 : a.tx3)[f] = x3_part(v, h);
+      continue;
+    }
     if (e < ns) {
       int i = 0;
       while (e >= a.soff[i + 1]) ++i;
@@ -152,10 +184,10 @@ __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> 
 
 template <typename T>
 int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, void* km, void* tkm,
-            hipStream_t s) {
+            void* x3, void* tx3, hipStream_t s) {
   PrepArgs<T> a{};
   a.L = net.n_hidden;
-  int64_t so = 0, wo = 0, ko = 0, to = 0;
+  int64_t so = 0, wo = 0, ko = 0, to = 0, xo = 0, yo = 0;
   for (int i = 0; i <= a.L + 1; ++i) {
     a.width[i] = net.width[i];
     a.gamma[i] = (const T*)net.bn_scale[i];
@@ -169,19 +201,27 @@ int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, void* km
     a.woff[i] = wo;
     a.koff[i] = ko;
     a.toff[i] = to;
+    a.xoff[i] = xo;
+    a.yoff[i] = yo;
     wo += (int64_t)net.width[i] * net.width[i + 1];
     ko += (int64_t)net.width[i + 1] * pad16(net.width[i]);
     to += (int64_t)net.width[i] * pad16(net.width[i + 1]);
+    xo += (int64_t)net.width[i + 1] * 64 * ((net.width[i] + 31) / 32);
+    yo += (int64_t)net.width[i] * 64 * ((net.width[i + 1] + 31) / 32);
   }
   a.woff[a.L + 1] = wo;
   a.koff[a.L + 1] = ko;
   a.toff[a.L + 1] = to;
+  a.xoff[a.L + 1] = xo;
+  a.yoff[a.L + 1] = yo;
+  a.x3 = (_Float16*)x3;
+  a.tx3 = (_Float16*)tx3;
   a.gscale = (T)gscale;
   a.scales = (T*)scales;
   a.wt = (T*)wt;
   a.km = (T*)km;
   a.tkm = (T*)tkm;
-  const int64_t total = so + (wt ? wo : 0) + (km ? ko : 0) + (tkm ? to : 0);
+  const int64_t total = so + (wt ? wo : 0) + (km ? ko : 0) + (tkm ? to : 0) + (x3 ? xo : 0) + (tx3 ? yo : 0);
   const unsigned g = (unsigned)std::min<int64_t>((total + kAdamThreads - 1) / kAdamThreads, 1024);
   hipLaunchKernelGGL(k_mlp_prepare<T>, dim3(g), dim3(kAdamThreads), 0, s, a);
   return (int)hipGetLastError();
@@ -190,9 +230,9 @@ int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, void* km
 }  // namespace
 
 int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
-                       void* km, void* tkm, hipStream_t s) {
-  return dtype == DPAC_F64 ? prepare<double>(net, gamma_scale, scales, wt, km, tkm, s)
-                           : prepare<float>(net, gamma_scale, scales, wt, km, tkm, s);
+                       void* km, void* tkm, void* x3, void* tx3, hipStream_t s) {
+  return dtype == DPAC_F64 ? prepare<double>(net, gamma_scale, scales, wt, km, tkm, nullptr, nullptr, s)
+                           : prepare<float>(net, gamma_scale, scales, wt, km, tkm, x3, tx3, s);
 }
 
 int adam_launch(int dtype, int n, const int64_t* numel, void* const* var, const void* const* grad,

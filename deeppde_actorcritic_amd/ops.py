@@ -114,7 +114,8 @@ class MlpView:
     `tensors` keeps every device buffer the struct points to alive; all must be
     contiguous, on the GPU, in the rollout's dtype."""
 
-    def __init__(self, scales, shifts, weights, bias, ekn_head: bool, weights_km=None):
+    def __init__(self, scales, shifts, weights, bias, ekn_head: bool, weights_km=None,
+                 weights_x3=None, weights_t_x3=None):
         L = len(weights) - 1
         if not 1 <= L <= _lib.MLP_MAX_HIDDEN:
             raise ValueError(f"the fused rollout supports 1..{_lib.MLP_MAX_HIDDEN} hidden layers, got {L}")
@@ -130,10 +131,17 @@ class MlpView:
         for i in range(L + 2):
             m.bn_scale[i], m.bn_shift[i] = sc[i].data_ptr(), sh[i].data_ptr()
         m.bias = b.data_ptr()
+        self.km, self.x3_fwd, self.x3_bwd = weights_km, weights_x3, weights_t_x3
+        self.halves = []
         if weights_km is not None:  # k-major images (dpac_mlp.weight_km), kept alive here
             self.tensors += list(weights_km)
             for i, w in enumerate(weights_km):
                 m.weight_km[i] = w.data_ptr()
+        for slot, imgs in (("weight_x3", weights_x3), ("weight_t_x3", weights_t_x3)):
+            if imgs is not None:  # split-fp16 images (dpac_mlp.weight_x3 / weight_t_x3): kept
+                self.halves += list(imgs)  # alive here, outside the same-dtype `tensors`
+                for i, w in enumerate(imgs):
+                    getattr(m, slot)[i] = w.data_ptr()
         self.struct = m
         self.widths = [m.width[i] for i in range(L + 2)]
 
@@ -148,6 +156,17 @@ class MlpView:
 # "on": float networks also get the k-major weight images (dpac_mlp.weight_km) the fused
 # rollout / BPTT read with 4 k per load; "off": the row-major path (test reference).
 WEIGHT_KM = os.environ.get("DPAC_WEIGHT_KM", "on")
+# Products of float networks: "x3" = split-fp16 MFMA (dpac_mlp.weight_x3: three
+# v_mfma_f32_16x16x32_f16 per 32-k step, f32-accurate) in the kernels that
+# have it (the row-parallel V / G networks); "f32" = v_mfma_f32_16x16x4_f32 everywhere.
+MLP_MATH = os.environ.get("DPAC_MLP_MATH", "f32")
+if MLP_MATH not in ("x3", "f32"):
+    raise ValueError(f"DPAC_MLP_MATH must be 'x3' or 'f32', got {MLP_MATH!r}")
+
+
+def _x3_halves(k, n):
+    """Halves of a split-fp16 image with n columns over K = k (dpac.h weight_x3)."""
+    return n * 64 * ((k + 31) // 32)
 
 
 def _k16(k):
@@ -169,6 +188,7 @@ def mlp_prepare(gam, bet, Ws, b, ekn: bool, want_wt: bool, want_km: bool = True)
     raw = MlpView(gam, bet, Ws, b, ekn)  # bn_scale slots point at the raw gammas
     kw = dict(dtype=ref.dtype, device=ref.device)
     km = want_km and WEIGHT_KM == "on" and ref.dtype == torch.float32
+    x3 = MLP_MATH == "x3" and ref.dtype == torch.float32
     S = torch.empty(sum(widths), **kw)
     nw = [widths[i] * widths[i + 1] for i in range(L1)]
     nk = [widths[i + 1] * _k16(widths[i]) for i in range(L1)]
@@ -176,14 +196,21 @@ def mlp_prepare(gam, bet, Ws, b, ekn: bool, want_wt: bool, want_km: bool = True)
     WT = torch.empty(sum(nw), **kw) if want_wt else None
     KM = torch.empty(sum(nk), **kw) if km else None
     TKM = torch.empty(sum(nt), **kw) if (km and want_wt) else None
+    nx = [_x3_halves(widths[i], widths[i + 1]) for i in range(L1)]
+    ny = [_x3_halves(widths[i + 1], widths[i]) for i in range(L1)]
+    hk = dict(dtype=torch.float16, device=ref.device)
+    X3 = torch.empty(sum(nx), **hk) if x3 else None
+    TX3 = torch.empty(sum(ny), **hk) if (x3 and want_wt) else None
     call("dpac_mlp_prepare", _dtype_id(ref), ctypes.byref(raw.struct), bn_rs_host(ref.dtype),
-         _ptr(S), _ptr(WT), _ptr(KM), _ptr(TKM), _stream(ref))
+         _ptr(S), _ptr(WT), _ptr(KM), _ptr(TKM), _ptr(X3), _ptr(TX3), _stream(ref))
 
     def split(buf, sizes, shapes):
         offs = np.cumsum([0] + sizes).tolist()
         return [buf[offs[i]:offs[i + 1]].view(*shapes[i]) for i in range(L1)]
     km_f = split(KM, nk, [(widths[i + 1], _k16(widths[i])) for i in range(L1)]) if km else None
-    view = MlpView(list(torch.split(S, widths)), bet, Ws, b, ekn, km_f)
+    x3_f = split(X3, nx, [(nx[i],) for i in range(L1)]) if X3 is not None else None
+    x3_b = split(TX3, ny, [(ny[i],) for i in range(L1)]) if TX3 is not None else None
+    view = MlpView(list(torch.split(S, widths)), bet, Ws, b, ekn, km_f, x3_f, x3_b)
     wt = split(WT, nw, [(widths[i + 1], widths[i]) for i in range(L1)]) if want_wt else None
     wt_km = split(TKM, nt, [(widths[i], _k16(widths[i + 1])) for i in range(L1)]) \
         if TKM is not None else None

@@ -50,8 +50,10 @@ extern "C" {
 #endif
 
 /* 2: dpac_rollout_nn_bwd / dpac_mlp_rows_bwd take weight_t_km (round 2); adds
- * dpac_rollout_nn_mask_bytes.  Bindings must refuse a library of another version. */
-#define DPAC_ABI_VERSION 2
+ * dpac_rollout_nn_mask_bytes.  3: dpac_mlp gains weight_x3 / weight_t_x3 (split-fp16
+ * images) and dpac_mlp_prepare writes them.  Bindings must refuse a library of another
+ * version. */
+#define DPAC_ABI_VERSION 3
 
 /* status codes besides hipError_t values */
 #define DPAC_OK 0
@@ -248,6 +250,17 @@ int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
  *     it and take the images of weight_t in their own `weight_t_km` argument, so
  *     one struct serves both directions.  dpac_mlp_prepare writes both kinds.
  *     The wide layers then load 4 k per lane and instruction.
+ *   weight_x3[i] / weight_t_x3[i] (optional, float only; NULL = not used): split-fp16
+ *     images of weight[i] (forward entry points) and of weight_t[i] (backward entry
+ *     points).  With every slot of a direction set, the float row kernels
+ *     (dpac_mlp_rows_fwd[_td1] / dpac_mlp_rows_bwd[_td1]) run the products on
+ *     v_mfma_f32_16x16x32_f16 as hi*hi + hi*lo + lo*hi of the operands' splits
+ *     a = hi + lo * 2^-12 (hi = fp16(a), lo = fp16((a - hi) * 2^12)), accumulated in
+ *     f32: f32-accurate products at 5.3x fewer MFMA cycles.  Image
+ *     layout, per output column n and 32-wide k chunk c: 32 halves hi then 32 halves lo
+ *     of column n of the operand, zero past K: [cols][ceil(K / 32)][64] halves, with
+ *     cols / K = width[i+1] / width[i] (forward) and width[i] / width[i+1] (backward).
+ *     Operand range: |activations| and the per-row scaled gradients below 65504.
  * 1 <= n_hidden <= DPAC_MLP_MAX_HIDDEN, every width <= DPAC_MLP_MAX_WIDTH.
  * Outputs as dpac_rollout_fwd, with u [N][B][c] the control actually applied.
  * y/disc (optional, both or neither): the pathwise cost in `cost_order`.
@@ -266,6 +279,8 @@ typedef struct dpac_mlp {
   const void* weight[DPAC_MLP_MAX_HIDDEN + 1];
   const void* bias;
   const void* weight_km[DPAC_MLP_MAX_HIDDEN + 1];
+  const void* weight_x3[DPAC_MLP_MAX_HIDDEN + 1];
+  const void* weight_t_x3[DPAC_MLP_MAX_HIDDEN + 1];
 } dpac_mlp;
 
 int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
@@ -401,9 +416,13 @@ int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, doubl
  * Optional k-major images (see dpac_mlp.weight_km), concatenated over i:
  * weight_km = [W_i^T padded: [width[i+1]][roundup(width[i], 16)]] (forward) and
  * weight_t_km = [(W_i ⊙ s_{i+1}) padded: [width[i]][roundup(width[i+1], 16)]]
- * (backward).  bn_shift, bias and net->weight_km are not read. */
+ * (backward).  Optional split-fp16 images (float only; see dpac_mlp.weight_x3), each
+ * concatenated over i: weight_x3 = [W_i as [width[i+1]][ceil(width[i]/32)][64] halves]
+ * and weight_t_x3 = [(W_i ⊙ s_{i+1})^T as [width[i]][ceil(width[i+1]/32)][64] halves].
+ * bn_shift, bias, net->weight_km and the x3 slots of net are not read. */
 int dpac_mlp_prepare(int32_t dtype, const dpac_mlp* net, double gamma_scale, void* scales,
-                     void* weight_t, void* weight_km, void* weight_t_km, void* stream);
+                     void* weight_t, void* weight_km, void* weight_t_km, void* weight_x3,
+                     void* weight_t_x3, void* stream);
 
 /* ---- optimizer step --------------------------------------------------
  * One step of TF-form Adam (the reference's tf.keras Adam, solver.py:16-21;

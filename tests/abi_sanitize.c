@@ -167,7 +167,7 @@ int main(void) {
   }
   expect_err(dpac_mlp_param_grads(DPAC_F32, 16, &m, 1.0, P, 20, P, P, P, 0, P, NULL), "param_grads: workspace 0 B");
   expect_err(dpac_mlp_param_grads(DPAC_F32, 16, NULL, 1.0, P, 20, P, P, P, 1 << 20, P, NULL), "param_grads: NULL mlp");
-  expect_err(dpac_mlp_prepare(DPAC_F32, NULL, 1.0, P, P, NULL, NULL, NULL), "prepare: NULL mlp");
+  expect_err(dpac_mlp_prepare(DPAC_F32, NULL, 1.0, P, P, NULL, NULL, NULL, NULL, NULL), "prepare: NULL mlp");
   int64_t numel[2] = {10, -4};
   void* vars[2] = {P, P};
   const void* grads[2] = {P, P};

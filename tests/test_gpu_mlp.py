@@ -278,7 +278,7 @@ def test_mlp_prepare_matches_tensor_ops(dtype):
     k16 = lambda k: (k + 15) // 16 * 16
     if dtype == torch.float32:  # k-major images: W_i^T and W_i * s_{i+1}, zero-padded K
         L1 = len(Ws)
-        km = view.tensors[-L1:]
+        km = view.km
         for i in range(L1):
             ref_f = torch.zeros(widths[i + 1], k16(widths[i]), dtype=dtype, device="cuda")
             ref_f[:, :widths[i]] = Ws[i].t()
@@ -288,3 +288,76 @@ def test_mlp_prepare_matches_tensor_ops(dtype):
             assert torch.equal(wt_km[i], ref_b)
     else:
         assert wt_km is None
+
+
+def _x3_image(M):
+    """The split-fp16 image (include/dpac.h dpac_mlp.weight_x3) of an operand M [K][cols]:
+    per column and 32-wide k chunk, 32 halves hi = fp16(M) then 32 halves lo =
+    fp16((M - hi) * 2^12), zero past K."""
+    K, n = M.shape
+    nch = (K + 31) // 32
+    P = torch.zeros(nch * 32, n, dtype=torch.float32, device=M.device)
+    P[:K] = M
+    hi = P.half()
+    lo = ((P - hi.float()) * 4096.0).half()
+    img = torch.stack([hi.t().reshape(n, nch, 32), lo.t().reshape(n, nch, 32)], 2)  # [n][nch][2][32]
+    return img.reshape(-1)
+
+
+def test_mlp_prepare_split_fp16_images(monkeypatch):
+    """dpac_mlp_prepare's split-fp16 images: bitwise the split of W_i (forward) and of
+    W_i * s_{i+1} (backward) formed with tensor ops; absent for float64 or DPAC_MLP_MATH=f32."""
+    monkeypatch.setattr(ops, "MLP_MATH", "x3")
+    widths = (20, 200, 130, 7, 21)
+    gen = torch.Generator().manual_seed(12)
+    gam = [torch.rand(w, generator=gen).cuda() for w in widths]
+    bet = [torch.randn(w, generator=gen).cuda() for w in widths]
+    Ws = [torch.randn(widths[i], widths[i + 1], generator=gen).cuda() * 0.1 for i in range(len(widths) - 1)]
+    b = torch.zeros(widths[-1], device="cuda")
+    view, wt, _ = ops.mlp_prepare(gam, bet, Ws, b, False, True)
+    rs = torch.rsqrt(torch.tensor(1.0 + 1e-6)).cuda()
+    s = [rs * g for g in gam]
+    for i in range(len(Ws)):
+        assert torch.equal(view.x3_fwd[i], _x3_image(Ws[i]))
+        assert torch.equal(view.x3_bwd[i], _x3_image((Ws[i] * s[i + 1]).t()))
+        assert view.struct.weight_x3[i] == view.x3_fwd[i].data_ptr()
+        assert view.struct.weight_t_x3[i] == view.x3_bwd[i].data_ptr()
+    v64, _, _ = ops.mlp_prepare([g.double() for g in gam], [t.double() for t in bet],
+                                [w.double() for w in Ws], b.double(), False, True)
+    assert v64.x3_fwd is None and v64.struct.weight_x3[0] is None
+    monkeypatch.setattr(ops, "MLP_MATH", "f32")
+    v32, _, _ = ops.mlp_prepare(gam, bet, Ws, b, False, True)
+    assert v32.x3_fwd is None and v32.x3_bwd is None
+
+
+@pytest.mark.parametrize("AC,name,d,hidden,R", ROW_CASES + [("critic_grad", "LQR", 20, (200, 200, 200), 63),
+                                                          ("critic", "EKN", 20, (256, 17), 65)])
+def test_row_mlp_split_fp16_vs_float64(AC, name, d, hidden, R, monkeypatch):
+    """The split-fp16 row kernels (dpac_mlp_x3.h) against the float64 statement of the same
+    network and the exact-f32 kernels: the forward, the saves, the input-gradient chain and
+    every parameter gradient within the float32 kernels' tolerances, and no further from the
+    float64 values than 2x the exact-f32 kernels' error (+ 1e-6)."""
+    net = net_pair(AC, name, d, hidden, torch.float32)
+    net64 = net_pair(AC, name, d, hidden, torch.float64)
+    with torch.no_grad():
+        for a, b in zip(net64.trainable_variables(), net.trainable_variables()):
+            a.copy_(b.double())
+    gen = torch.Generator(DEV).manual_seed(R + 3)
+    x = torch.randn(R, d, device=DEV, generator=gen) * 0.5
+    wgt = torch.randn(R, net.sizes[-1] - (1 if net.ekn_head else 0), device=DEV, generator=gen)
+
+    def run(model, xx, w):
+        xx = xx.clone().requires_grad_(True)
+        out = model(xx)
+        g = torch.autograd.grad(torch.sum(out * w) / R, [xx] + model.trainable_variables())
+        return [out.detach()] + list(g)
+
+    ref = torch_path(lambda: run(net64, x.double(), wgt.double()))
+    errs = {}
+    for math in ("f32", "x3"):
+        monkeypatch.setattr(ops, "MLP_MATH", math)
+        got = run(net, x, wgt)
+        errs[math] = [float((a.double() - r).abs().max()) / (1 + float(r.abs().max())) for a, r in zip(got, ref)]
+    print(f"\n[x3 rows {AC} {hidden} R={R}] max err f32 {max(errs['f32']):.2e} x3 {max(errs['x3']):.2e}")
+    for e32, ex3 in zip(errs["f32"], errs["x3"]):
+        assert ex3 <= 1e-4 and ex3 <= 2 * e32 + 1e-6
