@@ -159,7 +159,7 @@ WEIGHT_KM = os.environ.get("DPAC_WEIGHT_KM", "on")
 # Products of float networks: "x3" = split-fp16 MFMA (dpac_mlp.weight_x3: three
 # v_mfma_f32_16x16x32_f16 per 32-k step, f32-accurate) in the kernels that
 # have it (the row-parallel V / G networks); "f32" = v_mfma_f32_16x16x4_f32 everywhere.
-MLP_MATH = os.environ.get("DPAC_MLP_MATH", "f32")
+MLP_MATH = os.environ.get("DPAC_MLP_MATH", "x3")
 if MLP_MATH not in ("x3", "f32"):
     raise ValueError(f"DPAC_MLP_MATH must be 'x3' or 'f32', got {MLP_MATH!r}")
 
