@@ -1,21 +1,29 @@
 # Builds libdpac.so (gfx950) in-tree.  The oracle (oracle/) is Python (torch-CPU float64)
 # and needs no build.
 #   make -j8        -> deeppde_actorcritic_amd/libdpac.so
+# Each equation family's kernels are compiled once per dtype AND state dimension (one object
+# each, registered at load time: Registrar in dpac_kernels.h), so the heavy template
+# instantiations build in parallel.
 HIPCC     ?= /opt/rocm/bin/hipcc
 ARCH      ?= gfx950
 PKG       := deeppde_actorcritic_amd
 CSRC      := $(PKG)/csrc
 OBJDIR    := build/obj
-# state dimensions with compiled kernels (every shipped reference config: 4, 5, 10, 20)
+# state dimensions with compiled kernels (every shipped reference config: 4, 5, 10, 20);
+# VDP needs an even dimension
 DIMS      ?= 4,5,10,20
 DIMS_EVEN ?= 4,10,20
-HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) \
-             -DDPAC_DIMS=$(DIMS) -DDPAC_DIMS_EVEN=$(DIMS_EVEN) -Wno-pass-failed \
+comma     := ,
+DIM_LIST  := $(subst $(comma), ,$(DIMS))
+EVEN_LIST := $(subst $(comma), ,$(DIMS_EVEN))
+BASEFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wno-pass-failed \
              -ffp-contract=off
+HIPFLAGS  := $(BASEFLAGS) -DDPAC_DIMS=$(DIMS) -DDPAC_DIMS_EVEN=$(DIMS_EVEN)
 EQNS      := lqr lqrvar ekn vdp
 HDRS      := $(wildcard $(CSRC)/*.h) include/dpac.h
-OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_params.o \
-             $(foreach e,$(EQNS),$(OBJDIR)/dpac_eqn_$(e)_f32.o $(OBJDIR)/dpac_eqn_$(e)_f64.o)
+eqn_dims   = $(if $(filter vdp,$(1)),$(EVEN_LIST),$(DIM_LIST))
+EQN_OBJS  := $(foreach e,$(EQNS),$(foreach d,$(call eqn_dims,$(e)),$(foreach t,f32 f64,$(OBJDIR)/dpac_eqn_$(e)_$(t)_d$(d).o)))
+OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_params.o $(EQN_OBJS)
 LIB       := $(PKG)/libdpac.so
 
 .PHONY: all lib clean
@@ -34,13 +42,13 @@ $(OBJDIR)/dpac_params.o: $(CSRC)/dpac_params.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/dpac_eqn_%_f32.o: $(CSRC)/dpac_eqn_%.hip $(HDRS)
+# $(1) equation, $(2) f32 | f64, $(3) dimension
+define EQN_RULE
+$(OBJDIR)/dpac_eqn_$(1)_$(2)_d$(3).o: $(CSRC)/dpac_eqn_$(1).hip $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -DDPAC_TU_DOUBLE=0 -c $< -o $@
-
-$(OBJDIR)/dpac_eqn_%_f64.o: $(CSRC)/dpac_eqn_%.hip $(HDRS)
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -DDPAC_TU_DOUBLE=1 -c $< -o $@
+	$(HIPCC) $(BASEFLAGS) -DDPAC_DIMS=$(3) -DDPAC_DIMS_EVEN=$(3) -DDPAC_TU_DOUBLE=$(if $(filter f64,$(2)),1,0) -c $$< -o $$@
+endef
+$(foreach e,$(EQNS),$(foreach d,$(call eqn_dims,$(e)),$(foreach t,f32 f64,$(eval $(call EQN_RULE,$(e),$(t),$(d))))))
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)

@@ -77,18 +77,10 @@ def time_launches(launch, steps, warmup, world):
     return wall, per_launch_ms
 
 
-def time_launches_bracketed(launch, steps):
-    """Each of `steps` launches between its own HIP event pair (after the timed region, on
-    the same stream): the mean per-kernel duration without the dispatch gaps, the figure
-    rocprofv3's kernel trace reports (tools/rocprof_headline.py compares the two)."""
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    torch.cuda.synchronize()
-    for i, (a, b) in enumerate(evs):
-        a.record()
-        launch(i)
-        b.record()
-    torch.cuda.synchronize()
-    return float(np.mean([a.elapsed_time(b) for a, b in evs]))
+def progress(msg):
+    """One progress line on stderr (a long bench phase — the CPU baseline, the training
+    variants — must not look hung to a watchdog that reads the output)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def max_over_ranks(v, world):
@@ -144,6 +136,7 @@ def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total
     from deeppde_actorcritic_amd import solver as psol
     from deeppde_actorcritic_amd.config import baseline_config
     Bg = total or B
+    progress(f"training variant {name}: batch {Bg} ({B} per rank)")
     cfg = baseline_config(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", Bg, Bg, name=name)
     bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
     sp = psol.ActorCriticSolver(cfg, bsde, seed=1, sampler="device", parallel=par)
@@ -227,6 +220,7 @@ def cpu_baseline(seconds=8.0):
             el = time.perf_counter() - t0
             if el >= seconds or reps >= 50:
                 break
+        progress(f"cpu_baseline rollout {tag}: {reps} reps in {el:.1f} s")
         entries[f"rollout_{tag}"] = {
             "value": reps * B_PER_GPU * HORIZON / el, "unit": "traj-steps/s",
             "sample": f"{reps} x oracle propagate_adaptive(cheat=True), {tag}, B={B_PER_GPU}, d={DIM}, "
@@ -244,6 +238,7 @@ def cpu_baseline(seconds=8.0):
         so.train_step_critic(dc)
         so.train_step_actor(da)
         el = time.perf_counter() - t0
+        progress(f"cpu_baseline iteration {tag}: {el:.1f} s")
         entries[f"iteration_lqr_d20_{tag}"] = {
             "value": 2 * Bt * 100 / el, "unit": "traj-steps/s", "ms_per_iteration": el * 1e3,
             "sample": f"1 oracle training iteration (critic + actor step) on lqr_d20, {tag}, B={Bt}, "
@@ -262,6 +257,7 @@ def cpu_baseline(seconds=8.0):
         el = time.perf_counter() - t0
         if el >= seconds or reps >= 50:
             break
+    progress(f"cpu_baseline rollout f64 on {nproc} threads: {reps} reps in {el:.1f} s")
     entries["rollout_f64_all_cores"] = {
         "value": reps * B_PER_GPU * HORIZON / el, "unit": "traj-steps/s", "cores": nproc,
         "sample": f"{reps} x oracle propagate_adaptive(cheat=True), f64, B={B_PER_GPU}, d={DIM}, N={HORIZON}, "
@@ -320,11 +316,10 @@ def main():
     off = rank * B  # this rank's global trajectories [rank*B, rank*B + B)
     rs = RolloutSets(lib, eqp, scheme, dtype, B, N, d, off, N_SETS)
 
+    progress(f"headline: {args.warmup} + {args.steps} launches over {N_SETS} cold buffer sets")
     wall, per_launch_ms = time_launches(rs.launcher(N_SETS), args.steps, args.warmup, world)
     wall = max_over_ranks(wall, world)
     per_launch_ms = max_over_ranks(per_launch_ms, world)
-    # the same cold launches, each between its own event pair (kernel time without gaps)
-    kernel_ms = max_over_ranks(time_launches_bracketed(rs.launcher(N_SETS), args.steps), world)
     ms_per_step = wall / args.steps * 1e3
     value = world * B * N * args.steps / wall
     algo_bytes = B * N * (2 * d + 2) * esize
@@ -344,13 +339,12 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": tsrc, "kernel": "dpac::k_rollout_staged",
                      "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": per_launch_ms,
-                     "avg_kernel_ms_bracketed": kernel_ms,
-                     "frac_bracketed": algo_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "note": "achieved/frac: one event pair over the K timed launches (per-launch time "
-                             "incl. dispatch gaps); *_bracketed: each launch between its own event pair, "
-                             "the per-kernel duration rocprofv3 reports (profiles/r03_rocprof_headline.json)"},
+                     "note": "achieved = algorithmic bytes / (HIP event pair over the K timed launches / K) on "
+                             "the launch stream; rocprofv3's mean duration of the same cold launches agrees "
+                             "within 1% (tools/rocprof_headline.py -> profiles/r03_rocprof_headline.json)"},
     }
     if not args.no_variants:
+        progress("variants: MALL-resident, in-kernel Philox, float64, TD1, fused NN rollout")
         variants = {}
         k2 = max(20, args.steps // 4)
         # the same launch on ONE buffer set: inputs and outputs stay in the Infinity Cache
@@ -420,6 +414,7 @@ def main():
         del rs, nn_out
         torch.cuda.empty_cache()
         if not args.no_train:
+            progress("training-iteration variants")
             if world == 1:
                 # BASELINE configs[1], [2] (B = 4096 on one GPU), configs[4]'s per-GPU shard of
                 # 65536 over 8 GPUs, and the reference's shipped batch (configs/*.json: 2048)
@@ -438,6 +433,7 @@ def main():
             variants["training_dp_lqr_var_d20"] = v
         out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("cpu_baseline (oracle on the host cores, bounded samples)")
         out["cpu_baseline"] = cpu_baseline()
     elif rank == 0:
         out["cpu_baseline"] = None

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPAC_LIB", os.path.join(_HERE, "libdpac.so"))
 
 # constants mirrored from include/dpac.h
-ABI_VERSION = 3  # DPAC_ABI_VERSION: load() refuses a library built from another header
+ABI_VERSION = 4  # DPAC_ABI_VERSION: load() refuses a library built from another header
 DPAC_OK, DPAC_EINVAL, DPAC_EUNSUP = 0, -1, -2
 F32, F64 = 0, 1
 EQN_LQR, EQN_VDP, EQN_EKN, EQN_LQR_VAR = 0, 1, 2, 3

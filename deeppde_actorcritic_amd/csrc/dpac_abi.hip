@@ -8,18 +8,17 @@
 #include "dpac_kernels.h"
 
 namespace dpac {
-int dispatch_lqr_f32(const OpArgs&);
-int dispatch_vdp_f32(const OpArgs&);
-int dispatch_ekn_f32(const OpArgs&);
-int dispatch_lqrvar_f32(const OpArgs&);
-int dispatch_lqr_f64(const OpArgs&);
-int dispatch_vdp_f64(const OpArgs&);
-int dispatch_ekn_f64(const OpArgs&);
-int dispatch_lqrvar_f64(const OpArgs&);
-bool has_dim_lqr(int);
-bool has_dim_vdp(int);
-bool has_dim_ekn(int);
-bool has_dim_lqrvar(int);
+// The instantiation table the equation TUs fill at load time (Registrar, dpac_kernels.h):
+// [equation id][dim][f64].  Zero-initialised before any constructor runs.
+constexpr int kMaxRegDim = 64;
+static DispatchFn g_dispatch[4][kMaxRegDim + 1][2];
+void register_dispatch(int eqn, int dim, int f64, DispatchFn fn) {
+  if (eqn >= 0 && eqn < 4 && dim >= 1 && dim <= kMaxRegDim && (f64 == 0 || f64 == 1)) g_dispatch[eqn][dim][f64] = fn;
+}
+DispatchFn find_dispatch(int eqn, int dim, int f64) {
+  if (eqn < 0 || eqn >= 4 || dim < 1 || dim > kMaxRegDim || (f64 != 0 && f64 != 1)) return nullptr;
+  return g_dispatch[eqn][dim][f64];
+}
 int64_t mlp_param_grads_ws_bytes(int dtype, int64_t rows, const dpac_mlp& net);
 int mlp_param_grads_launch(int dtype, int64_t rows, const dpac_mlp& net, double gamma_scale,
                            const void* x, int64_t ldx, const void* z, const void* G, void* ws,
@@ -74,13 +73,7 @@ int check_eq(const dpac_eqn_params* eq) {
       return fail(DPAC_EINVAL, "unknown equation id %d", eq->eqn);
   }
   if (!(eq->R > 0)) return fail(DPAC_EINVAL, "R must be > 0");
-  bool has = false;
-  switch (eq->eqn) {
-    case DPAC_EQN_LQR: has = has_dim_lqr(eq->dim); break;
-    case DPAC_EQN_VDP: has = has_dim_vdp(eq->dim); break;
-    case DPAC_EQN_EKN: has = has_dim_ekn(eq->dim); break;
-    case DPAC_EQN_LQR_VAR: has = has_dim_lqrvar(eq->dim); break;
-  }
+  const bool has = find_dispatch(eq->eqn, eq->dim, 0) && find_dispatch(eq->eqn, eq->dim, 1);
   if (!has)
     return fail(DPAC_EUNSUP, "equation %d has no kernel instantiation for dim %d", eq->eqn,
                 eq->dim);
@@ -179,12 +172,8 @@ int launch(const OpArgs& a) {
     return fail(DPAC_EINVAL, "batch too large for one launch: every [N+1][B][d] array must stay "
                 "below 2 GiB (B=%lld, N=%d, d=%d); split the batch over launches with "
                 "traj_offset", (long long)a.B, a.N, a.eq.dim);
-  switch (a.eq.eqn) {
-    case DPAC_EQN_LQR: r = f64 ? dispatch_lqr_f64(a) : dispatch_lqr_f32(a); break;
-    case DPAC_EQN_VDP: r = f64 ? dispatch_vdp_f64(a) : dispatch_vdp_f32(a); break;
-    case DPAC_EQN_EKN: r = f64 ? dispatch_ekn_f64(a) : dispatch_ekn_f32(a); break;
-    case DPAC_EQN_LQR_VAR: r = f64 ? dispatch_lqrvar_f64(a) : dispatch_lqrvar_f32(a); break;
-  }
+  const DispatchFn fn = find_dispatch(a.eq.eqn, a.eq.dim, f64 ? 1 : 0);
+  r = fn ? fn(a) : DPAC_EUNSUP;
   if (r == DPAC_EUNSUP) return fail(r, "no kernel for equation %d dim %d", a.eq.eqn, a.eq.dim);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();
@@ -380,7 +369,9 @@ int64_t dpac_rollout_nn_mask_bytes(const dpac_mlp* actor, int32_t dtype, int64_t
   const int tile = nn_tile_rows();
   if (tile == 4 || (tile == 0 && num_sample <= 1024)) return 0;
   const int L = actor->n_hidden;
-  if (!nn_fast_host<float>(L, actor->width, actor->weight_km, actor->width[0], actor->width[L + 1])) return 0;
+  if (!nn_fast_host<float>(L, actor->width, actor->weight_km, actor->width[0], actor->width[L + 1]) &&
+      !nn_x3_host(L, actor->width, actor->weight_x3, actor->width[0], actor->width[L + 1]))
+    return 0;
   return (int64_t)num_steps * ((num_sample + 15) / 16) * nn_mask_tile_bytes(L);
 }
 

@@ -1,15 +1,12 @@
-// Kernel instantiations for the ekn equation family (equation.py, class ekn),
-// compiled once per dtype: -DDPAC_TU_DOUBLE=0 (float) / 1 (double).
+// Kernel instantiations for the ekn equation family (equation.py, class ekn) for one
+// dtype (-DDPAC_TU_DOUBLE=0 float / 1 double) and the state dimensions in DPAC_DIMS
+// (the Makefile builds one object per dimension); they register with dpac_abi.hip's table.
 #include "dpac_kernels.h"
 
 namespace dpac {
 template <typename T, int D>
 using EqEKNFor = EqEKN<T, D, eqn_lanes(DPAC_EQN_EKN, D)>;
-using eknDims = DimList<EqEKNFor, DPAC_DIMS>;
-#if DPAC_TU_DOUBLE
-int dispatch_ekn_f64(const OpArgs& a) { return eknDims::dispatch<double>(a); }
-#else
-int dispatch_ekn_f32(const OpArgs& a) { return eknDims::dispatch<float>(a); }
-bool has_dim_ekn(int d) { return eknDims::has(d); }
-#endif
+namespace {
+const Registrar<EqEKNFor, std::conditional_t<DPAC_TU_DOUBLE, double, float>, DPAC_DIMS> reg(DPAC_EQN_EKN);
+}  // namespace
 }  // namespace dpac

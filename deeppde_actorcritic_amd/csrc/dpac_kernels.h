@@ -1054,6 +1054,7 @@ __global__ __launch_bounds__(64) void k_eval(const E eq, const DevConsts<T> c, i
 #include "dpac_rollout_nn.h"
 #include "dpac_rollout_nn_bwd.h"
 #include "dpac_rollout_nn4.h"
+#include "dpac_rollout_nn_x3.h"
 
 // ---------------------------------------------------------------------------
 // Launcher for one (T, equation functor, D).
@@ -1256,6 +1257,19 @@ int run_op(const OpArgs& a) {
       r.mask = r.fast ? a.mask_in : nullptr;
       r.mb = nn_mask_tile_bytes(m.L);
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
+      if constexpr (kFastOk) {  // split-fp16 chain (dpac_rollout_nn_x3.h): needs the forward's mask
+        if (r.mask && bptt_kernel() == 2 &&
+            nn_x3_host(m.L, m.width, (const void* const*)a.mlp.weight_t_x3, m.width[m.L + 1], m.width[0])) {
+          for (int i = 0; i <= m.L; ++i) r.wtx3[i] = (const _Float16*)a.mlp.weight_t_x3[i];
+          auto kfn = adaptive ? k_rollout_nn_bwd_x3<E, D, DPAC_SCHEME_ADAPTIVE>
+                              : k_rollout_nn_bwd_x3<E, D, DPAC_SCHEME_NAIVE>;
+          if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)NxLds::total))
+            return (int)e;
+          hipLaunchKernelGGL(kfn, ngrid, nblock, NxLds::total, s, eq, c, m, r);
+          break;
+        }
+      }
       if (bptt_kernel() == 2) {
         int wsum = 0;
         for (int i = 0; i <= m.L + 1; ++i) wsum += m.width[i];
@@ -1344,9 +1358,39 @@ int run_op(const OpArgs& a) {
         }
       }
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
-      if (m.fast && a.save_mask && a.save_z) {  // the 16-row fast path writes the sign bits
+      bool x3 = false;
+      if constexpr (kFastOk)
+        x3 = nn_x3_host(m.L, m.width, (const void* const*)a.mlp.weight_x3, m.width[0], m.width[m.L + 1]);
+      if ((m.fast || x3) && a.save_mask && a.save_z) {  // the 16-row fast paths write the sign bits
         r.save_mask = a.save_mask;
         if (a.mask_written) *a.mask_written = 1;
+      }
+      if constexpr (kFastOk) {  // split-fp16 MLP (dpac_rollout_nn_x3.h)
+        if (x3) {
+          for (int i = 0; i <= m.L; ++i) m.wx3[i] = (const _Float16*)a.mlp.weight_x3[i];
+          const bool save = r.save_z != nullptr, mask = r.save_mask != nullptr;
+          hipError_t e = hipSuccess;
+#define DPAC_NX_LAUNCH(SCH, CO, SV, MK)                                                                    \
+  {                                                                                                       \
+    auto kfn = k_rollout_nn_x3<E, D, SCH, CO, SV, MK>;                                                    \
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            (int)NxLds::total);                                                           \
+    if (e == hipSuccess) hipLaunchKernelGGL(kfn, ngrid, nblock, NxLds::total, s, eq, c, m, r);            \
+  }
+#define DPAC_NX_SV(SCH, CO)                                    \
+  if (mask) DPAC_NX_LAUNCH(SCH, CO, true, true)                \
+  else if (save) DPAC_NX_LAUNCH(SCH, CO, true, false)          \
+  else DPAC_NX_LAUNCH(SCH, CO, false, false)
+          if (adaptive) {
+            if (cost) { DPAC_NX_SV(DPAC_SCHEME_ADAPTIVE, true) } else { DPAC_NX_SV(DPAC_SCHEME_ADAPTIVE, false) }
+          } else {
+            if (cost) { DPAC_NX_SV(DPAC_SCHEME_NAIVE, true) } else { DPAC_NX_SV(DPAC_SCHEME_NAIVE, false) }
+          }
+#undef DPAC_NX_SV
+#undef DPAC_NX_LAUNCH
+          if (e != hipSuccess) return (int)e;
+          break;
+        }
       }
 #define DPAC_ROLL_NN(SCH, CO)                                                                                   \
   do {                                                                                                          \
@@ -1369,21 +1413,19 @@ int run_op(const OpArgs& a) {
   return (int)hipGetLastError();
 }
 
-// Dispatch over the compiled dimensions of one equation family for one dtype.
+// Kernel instantiations register themselves per (equation family, dim, dtype): each
+// equation TU is compiled once per dtype and state dimension (Makefile), so the heavy
+// template instantiations build in parallel, and dpac_abi.hip finds them in a table.
 // EQ<T, D> is the functor with its lane split already chosen.
-template <template <typename, int> class EQ, int... Ds>
-struct DimList {
-  template <typename T, int D0, int... Rest>
-  static int go(const OpArgs& a) {
-    if (a.eq.dim == D0) return run_op<T, EQ<T, D0>, D0>(a);
-    if constexpr (sizeof...(Rest) > 0) return go<T, Rest...>(a);
-    return DPAC_EUNSUP;
+using DispatchFn = int (*)(const OpArgs&);
+void register_dispatch(int eqn, int dim, int f64, DispatchFn fn);
+DispatchFn find_dispatch(int eqn, int dim, int f64);
+
+template <template <typename, int> class EQ, typename T, int... Ds>
+struct Registrar {
+  explicit Registrar(int eqn) {
+    (register_dispatch(eqn, Ds, std::is_same<T, double>::value ? 1 : 0, &run_op<T, EQ<T, Ds>, Ds>), ...);
   }
-  template <typename T>
-  static int dispatch(const OpArgs& a) {
-    return go<T, Ds...>(a);
-  }
-  static bool has(int d) { return ((d == Ds) || ...); }
 };
 
 }  // namespace dpac

@@ -23,8 +23,11 @@
 // Layouts.  A row's activations live in LDS as 32-wide k chunks of 64 halves,
 // [hi(k0..k0+31) | lo(k0..k0+31)], row stride kX3Ld halves (264 dwords = 8 mod 64:
 // conflict-free ds_read_b128 as in dpac_mlp_rows.h).  The weight images
-// (dpac_mlp.weight_x3 / weight_t_x3, written by dpac_mlp_prepare) hold, per output
-// feature n and chunk c, the same 64 halves of column n of W (k-major).
+// (dpac_mlp.weight_x3 / weight_t_x3, written by dpac_mlp_prepare) are fragment-major:
+// per 16-feature tile, chunk and part (hi, lo) the 64 lanes' A operands, lane-ordered, so
+// one buffer_load_dwordx4 of a wave reads 1 KB of contiguous memory (8 cache lines; the
+// feature-major image of round 3's first build touched 16 half-used lines per quarter-wave,
+// and in the fused NN rollout those loads, not the MFMAs, set the step time).
 //
 // Workgroup: 8 wavefronts over kX3Rows = 64 rows (4 row tiles); the waves split the
 // 16-feature tiles (wave, wave + 8); every weight fragment serves the 4 row tiles, so the
@@ -143,19 +146,21 @@ __device__ __forceinline__ void x3_layer_t(const _Float16* in, int K, int Nout, 
                                            int lane, EPI& epi) {
   const int col_l = lane & 15, q = lane >> 4;
   const int nch = NCH ? NCH : x3_chunks(K);
-  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wx3, (uint32_t)(Nout * nch * 128));
+  const int ntiles = (Nout + 15) / 16;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wx3, (uint32_t)(ntiles * nch * 2048));
   uint32_t voff[NT];
   x3f4 ah[kX3RT][NT], al[kX3RT][NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    const int feat = (wave + kX3Waves * j) * 16 + col_l;
-    voff[j] = feat < Nout ? (uint32_t)(feat * nch * 128 + 16 * q) : kOOB;
+    const int tile = wave + kX3Waves * j;
+    voff[j] = tile < ntiles ? (uint32_t)(tile * nch * 2048 + 16 * lane) : kOOB;
 #pragma unroll
     for (int rt = 0; rt < kX3RT; ++rt) ah[rt][j] = al[rt][j] = x3f4{0, 0, 0, 0};
   }
-  auto loadW = [&](int c, int j, int part) {  // part 0: hi, 1: lo
+  (void)col_l;
+  auto loadW = [&](int c, int j, int part) {  // part 0: hi, 1: lo; one contiguous KB per wave
     return __builtin_bit_cast(x3h8, __builtin_amdgcn_raw_buffer_load_b128(
-                                        rW, (int)(voff[j] + (uint32_t)(c * 128 + 64 * part)), 0, 0));
+                                        rW, (int)(voff[j] + (uint32_t)(c * 2048 + 1024 * part)), 0, 0));
   };
   const _Float16* arow = in + col_l * kX3Ld + 8 * q;
   auto loadX = [&](int c, int rt, int part) {

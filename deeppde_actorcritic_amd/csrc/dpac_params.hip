@@ -113,12 +113,11 @@ struct PrepArgs {
 
 __device__ __forceinline__ int k16(int k) { return (k + 15) / 16 * 16; }
 
-// element h (0..63) of chunk c of a split-fp16 column (dpac.h dpac_mlp.weight_x3): the hi
-// (h < 32) or lo half of operand value v at k = 32c + (h & 31); hi = fp16(v),
-// lo = fp16((v - hi) * 2^12), as dpac_mlp_x3.h splits activations.
-__device__ __forceinline__ _Float16 x3_part(float v, int h) {
+// part 0 (hi) or 1 (lo) of operand value v in a split-fp16 image (dpac.h dpac_mlp.weight_x3):
+// hi = fp16(v), lo = fp16((v - hi) * 2^12), as dpac_mlp_x3.h splits activations.
+__device__ __forceinline__ _Float16 x3_part(float v, int part) {
   const _Float16 hi = (_Float16)v;
-  return h < 32 ? hi : (_Float16)((v - (float)hi) * 4096.f);
+  return part == 0 ? hi : (_Float16)((v - (float)hi) * 4096.f);
 }
 
 template <typename T>
@@ -132,7 +131,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> 
   const int64_t n4 = ns + nw + nk + nt;
   for (int64_t e = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; e < n4 + nx + ny;
        e += (int64_t)gridDim.x * kAdamThreads) {
-    if (e >= n4) {  // split-fp16 images: [cols][ceil(K/32)][64] halves per layer
+    if (e >= n4) {  // split-fp16 images, fragment-major: [tile][chunk][hi|lo][lane][8] halves per layer
       const bool fwd = e < n4 + nx;
       const int64_t f = fwd ? e - n4 : e - n4 - nx;
       const int64_t* off = fwd ? a.xoff : a.yoff;
@@ -140,13 +139,16 @@ __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> 
       while (f >= off[i + 1]) ++i;
       const int64_t r = f - off[i];
       const int K = fwd ? a.width[i] : a.width[i + 1], nch = (K + 31) / 32;
-      const int64_t n = r / (64 * nch), c = (r / 64) % nch;
-      const int h = (int)(r % 64), k = 32 * (int)c + (h & 31);
+      const int cols = fwd ? a.width[i + 1] : a.width[i];
+      const int64_t tc = r / 1024;                       // (tile, chunk)
+      const int t = (int)(tc / nch), c = (int)(tc % nch);
+      const int part = (int)(r / 512) & 1, lane = (int)(r / 8) & 63, el = (int)(r & 7);
+      const int n = 16 * t + (lane & 15), k = 32 * c + 8 * (lane >> 4) + el;
       float v = 0.f;
-      if (k < K)  // forward: W_i[k][n]; backward: W_i[n][k] * s_{i+1}[k] (as tkm_i)
+      if (k < K && n < cols)  // forward: W_i[k][n]; backward: W_i[n][k] * s_{i+1}[k] (as tkm_i)
         v = fwd ? (float)a.W[i][(int64_t)k * a.width[i + 1] + n]
-                : (float)(a.W[i][n * K + k] * (a.gscale * a.gamma[i + 1][k]));
-      (fwd ? a.x3 : a.tx3)[f] = x3_part(v, h);
+                : (float)(a.W[i][(int64_t)n * K + k] * (a.gscale * a.gamma[i + 1][k]));
+      (fwd ? a.x3 : a.tx3)[f] = x3_part(v, part);
       continue;
     }
     if (e < ns) {
@@ -206,8 +208,8 @@ int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, void* km
     wo += (int64_t)net.width[i] * net.width[i + 1];
     ko += (int64_t)net.width[i + 1] * pad16(net.width[i]);
     to += (int64_t)net.width[i] * pad16(net.width[i + 1]);
-    xo += (int64_t)net.width[i + 1] * 64 * ((net.width[i] + 31) / 32);
-    yo += (int64_t)net.width[i] * 64 * ((net.width[i + 1] + 31) / 32);
+    xo += (int64_t)((net.width[i + 1] + 15) / 16) * 1024 * ((net.width[i] + 31) / 32);
+    yo += (int64_t)((net.width[i] + 15) / 16) * 1024 * ((net.width[i + 1] + 31) / 32);
   }
   a.woff[a.L + 1] = wo;
   a.koff[a.L + 1] = ko;

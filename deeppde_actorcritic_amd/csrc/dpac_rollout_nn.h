@@ -78,6 +78,7 @@ struct NnMlp {
   const T* wkm[DPAC_MLP_MAX_HIDDEN + 1];  // k-major images of weight (optional, float)
   const T* bias;
   int fast;  // the actor-shape fast path applies (nn_fast_host)
+  const _Float16* wx3[DPAC_MLP_MAX_HIDDEN + 1];  // split-fp16 images of weight (k_rollout_nn_x3)
 };
 
 template <typename T>
@@ -872,6 +873,7 @@ struct NnBackArgs {
   int fast;  // the actor-shape fast path applies to the transposed chain (nn_fast_host)
   const uint8_t* mask;  // optional (fast path): the forward's sign bits, [N][ceil(B/16)][mb]
   int mb;
+  const _Float16* wtx3[DPAC_MLP_MAX_HIDDEN + 1];  // split-fp16 images of wt (k_rollout_nn_bwd_x3)
 };
 
 // The actor's BPTT through a fused NN rollout, as one launch: the reverse time

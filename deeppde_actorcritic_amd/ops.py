@@ -165,8 +165,9 @@ if MLP_MATH not in ("x3", "f32"):
 
 
 def _x3_halves(k, n):
-    """Halves of a split-fp16 image with n columns over K = k (dpac.h weight_x3)."""
-    return n * 64 * ((k + 31) // 32)
+    """Halves of a split-fp16 image with n columns over K = k (dpac.h weight_x3: 16-column
+    tiles x 32-k chunks x 1024 halves)."""
+    return (n + 15) // 16 * 1024 * ((k + 31) // 32)
 
 
 def _k16(k):

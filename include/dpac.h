@@ -51,9 +51,11 @@ extern "C" {
 
 /* 2: dpac_rollout_nn_bwd / dpac_mlp_rows_bwd take weight_t_km (round 2); adds
  * dpac_rollout_nn_mask_bytes.  3: dpac_mlp gains weight_x3 / weight_t_x3 (split-fp16
- * images) and dpac_mlp_prepare writes them.  Bindings must refuse a library of another
+ * images) and dpac_mlp_prepare writes them.  4: the split-fp16 images are fragment-major
+ * (below) and the float fused rollout / BPTT (dpac_rollout_nn_fwd[_masked],
+ * dpac_rollout_nn_bwd_masked) read them too.  Bindings must refuse a library of another
  * version. */
-#define DPAC_ABI_VERSION 3
+#define DPAC_ABI_VERSION 4
 
 /* status codes besides hipError_t values */
 #define DPAC_OK 0
@@ -253,13 +255,16 @@ int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
  *   weight_x3[i] / weight_t_x3[i] (optional, float only; NULL = not used): split-fp16
  *     images of weight[i] (forward entry points) and of weight_t[i] (backward entry
  *     points).  With every slot of a direction set, the float row kernels
- *     (dpac_mlp_rows_fwd[_td1] / dpac_mlp_rows_bwd[_td1]) run the products on
- *     v_mfma_f32_16x16x32_f16 as hi*hi + hi*lo + lo*hi of the operands' splits
- *     a = hi + lo * 2^-12 (hi = fp16(a), lo = fp16((a - hi) * 2^12)), accumulated in
- *     f32: f32-accurate products at 5.3x fewer MFMA cycles.  Image
- *     layout, per output column n and 32-wide k chunk c: 32 halves hi then 32 halves lo
- *     of column n of the operand, zero past K: [cols][ceil(K / 32)][64] halves, with
- *     cols / K = width[i+1] / width[i] (forward) and width[i] / width[i+1] (backward).
+ *     (dpac_mlp_rows_fwd[_td1] / dpac_mlp_rows_bwd[_td1]) and, for the actor-shape
+ *     networks (d, out <= 32, hidden layers 193..208 wide), the fused rollout and its
+ *     BPTT run the products on v_mfma_f32_16x16x32_f16 as hi*hi + hi*lo + lo*hi of the
+ *     operands' splits a = hi + lo * 2^-12 (hi = fp16(a), lo = fp16((a - hi) * 2^12)),
+ *     accumulated in f32: f32-accurate products at 5.3x fewer MFMA cycles (DESIGN.md
+ *     §4.3).  Image layout (fragment-major: one 64-lane 16-byte load reads 1 KB of
+ *     contiguous memory), with cols / K = width[i+1] / width[i] (forward) and
+ *     width[i] / width[i+1] (backward): [ceil(cols / 16)][ceil(K / 32)][2][64][8] halves,
+ *     element [t][c][p][l][e] = part p (0 hi, 1 lo) of the operand at column
+ *     n = 16 t + (l % 16), k = 32 c + 8 (l / 16) + e, zero where n >= cols or k >= K.
  *     Operand range: |activations| and the per-row scaled gradients below 65504.
  * 1 <= n_hidden <= DPAC_MLP_MAX_HIDDEN, every width <= DPAC_MLP_MAX_WIDTH.
  * Outputs as dpac_rollout_fwd, with u [N][B][c] the control actually applied.
@@ -417,8 +422,9 @@ int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, doubl
  * weight_km = [W_i^T padded: [width[i+1]][roundup(width[i], 16)]] (forward) and
  * weight_t_km = [(W_i ⊙ s_{i+1}) padded: [width[i]][roundup(width[i+1], 16)]]
  * (backward).  Optional split-fp16 images (float only; see dpac_mlp.weight_x3), each
- * concatenated over i: weight_x3 = [W_i as [width[i+1]][ceil(width[i]/32)][64] halves]
- * and weight_t_x3 = [(W_i ⊙ s_{i+1})^T as [width[i]][ceil(width[i+1]/32)][64] halves].
+ * concatenated over i in dpac_mlp.weight_x3's layout: weight_x3 = [W_i: ceil(width[i+1]/16)
+ * x ceil(width[i]/32) x 1024 halves] and weight_t_x3 = [(W_i ⊙ s_{i+1})^T: ceil(width[i]/16)
+ * x ceil(width[i+1]/32) x 1024 halves].
  * bn_shift, bias, net->weight_km and the x3 slots of net are not read. */
 int dpac_mlp_prepare(int32_t dtype, const dpac_mlp* net, double gamma_scale, void* scales,
                      void* weight_t, void* weight_km, void* weight_t_km, void* weight_x3,

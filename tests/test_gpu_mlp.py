@@ -292,16 +292,17 @@ def test_mlp_prepare_matches_tensor_ops(dtype):
 
 def _x3_image(M):
     """The split-fp16 image (include/dpac.h dpac_mlp.weight_x3) of an operand M [K][cols]:
-    per column and 32-wide k chunk, 32 halves hi = fp16(M) then 32 halves lo =
-    fp16((M - hi) * 2^12), zero past K."""
+    hi = fp16(M), lo = fp16((M - hi) * 2^12), zero past K and cols, fragment-major
+    [tile][chunk][hi|lo][lane][8]: element (t, c, p, l, e) holds column 16 t + l % 16 at
+    k = 32 c + 8 (l // 16) + e."""
     K, n = M.shape
-    nch = (K + 31) // 32
-    P = torch.zeros(nch * 32, n, dtype=torch.float32, device=M.device)
-    P[:K] = M
+    nch, nt = (K + 31) // 32, (n + 15) // 16
+    P = torch.zeros(nch * 32, nt * 16, dtype=torch.float32, device=M.device)
+    P[:K, :n] = M
     hi = P.half()
     lo = ((P - hi.float()) * 4096.0).half()
-    img = torch.stack([hi.t().reshape(n, nch, 32), lo.t().reshape(n, nch, 32)], 2)  # [n][nch][2][32]
-    return img.reshape(-1)
+    X = torch.stack([hi, lo]).reshape(2, nch, 4, 8, nt, 16)  # (p, c, q, e, t, r)
+    return X.permute(4, 1, 0, 2, 5, 3).reshape(-1)         # (t, c, p, q, r, e)
 
 
 def test_mlp_prepare_split_fp16_images(monkeypatch):

@@ -284,6 +284,7 @@ def test_fp32_kmajor_weights_match_row_major(name, d, hidden, B, monkeypatch):
     eqp = ep.params()
     x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=23, dtype=torch.float32, device=DEV)
     monkeypatch.setenv("DPAC_NN_TILE", "16")
+    monkeypatch.setenv("DPAC_NN_X3", "0")  # the f32 kernels (the x3 ones ignore weight_km)
     out, grads = {}, {}
     for km in ("on", "off"):
         monkeypatch.setattr(ops, "WEIGHT_KM", km)
@@ -379,11 +380,12 @@ def test_actor_fast_path_bitwise(name, d, hidden, B, scheme):
     widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
     view, wt, wt_km = ops.mlp_prepare(gam, bet, Ws, b, net.ekn_head, True)
     g_y = torch.full((B,), 1.0 / B, device=DEV)
-    keys = ("DPAC_NN_FAST", "DPAC_NN_TILE")
+    keys = ("DPAC_NN_FAST", "DPAC_NN_TILE", "DPAC_NN_X3")
     old = {k: os.environ.get(k) for k in keys}
     fwd, bwd = {}, {}
     try:
         os.environ["DPAC_NN_TILE"] = "16"
+        os.environ["DPAC_NN_X3"] = "0"  # the f32 kernels' two layer codes
         for f in ("0", "1"):
             os.environ["DPAC_NN_FAST"] = f
             fwd[f] = [t.clone() if torch.is_tensor(t) else [s.clone() for s in t[:3]]
@@ -431,6 +433,7 @@ def test_bptt_sign_mask_bitwise(name, d, hidden, B, scheme, monkeypatch):
     view, wt, wt_km = ops.mlp_prepare(gam, bet, Ws, b, net.ekn_head, True)
     monkeypatch.setenv("DPAC_NN_TILE", "16")
     monkeypatch.setenv("DPAC_NN_FAST", "1")
+    monkeypatch.setenv("DPAC_NN_X3", "0")  # the f32 pair (the x3 pair: test_gpu_nn_x3.py)
     fwd = {}
     for m in (False, True):
         monkeypatch.setattr(ops, "MASK_BPTT", m)

@@ -17,9 +17,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-FWD_POINTS = {0: "top", 10: "l0 A", 11: "l0 mfma", 1: "l0 done", 2: "l0 bar", 3: "l1 done", 4: "l1 bar", 5: "l2 done", 6: "l2 bar",
+FWD_POINTS = {0: "top", 10: "l0 A", 11: "l0 mfma", 12: "l1 mfma (x3)", 13: "l2 mfma (x3)", 1: "l0 done", 2: "l0 bar", 3: "l1 done", 4: "l1 bar", 5: "l2 done", 6: "l2 bar",
               7: "l3 done", 8: "l3 bar", 15: "step done"}
-BWD_POINTS = {0: "top", 1: "vjp done", 2: "vjp bar", 3: "l3 done", 4: "l3 bar", 5: "l2 done", 6: "l2 bar",
+BWD_POINTS = {0: "top", 12: "l1 mfma (x3)", 13: "l2 mfma (x3) / end", 1: "vjp done", 2: "vjp bar", 3: "l3 done", 4: "l3 bar", 5: "l2 done", 6: "l2 bar",
               7: "l1 done", 8: "l1 bar", 9: "l0 done", 10: "l0 bar", 13: "end", 14: "end bar"}
 
 

@@ -10,8 +10,8 @@ bench line the same command printed:
         --steps K --warmup W > profiles/r03_rocprof_headline.json
 
 bench.py launches dpac::k_rollout_staged<float, ...> (f32, LQR d = 20, no cost / u outputs) in
-this order: W warm-up + K timed + K bracketed launches over the 5 cold sets, then 5 warm-up
-+ k2 = max(20, K // 4) timed launches of the one-set (MALL-resident) variant.
+this order: W warm-up + K timed launches over the 5 cold sets, then 5 warm-up + k2 =
+max(20, K // 4) timed launches of the one-set (MALL-resident) variant.
 """
 import argparse
 import csv
@@ -34,22 +34,20 @@ def main():
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]  # us
     W, K = a.warmup, a.steps
     k2 = max(20, K // 4)
-    cold_t, cold_b = dur[W:W + K], dur[W + K:W + 2 * K]
-    mall = dur[W + 2 * K + 5:W + 2 * K + 5 + k2]
-    assert len(dur) == W + 2 * K + 5 + k2, (len(dur), W, K, k2)
+    cold = dur[W:W + K]
+    mall = dur[W + K + 5:W + K + 5 + k2]
+    assert len(dur) == W + K + 5 + k2, (len(dur), W, K, k2)
     algo = B * N * (2 * D + 2) * 4
     frac = lambda us: algo / (us * 1e-6) / 1e9 / HBM
     line = [json.loads(l) for l in open(a.bench_log) if l.startswith("{")][-1]
     rf = line["roofline"]
     out = {"kernel": rows[0]["Kernel_Name"][:120], "dispatches": len(dur),
-           "rocprof_cold_timed_mean_us": statistics.mean(cold_t), "rocprof_cold_bracketed_mean_us": statistics.mean(cold_b),
-           "rocprof_cold_mean_us": statistics.mean(cold_t + cold_b), "rocprof_mall_mean_us": statistics.mean(mall),
-           "frac_rocprof_cold": frac(statistics.mean(cold_t + cold_b)), "frac_rocprof_mall": frac(statistics.mean(mall)),
-           "bench_same_run": {"avg_launch_us": rf["avg_launch_ms"] * 1e3, "frac": rf["frac"],
-                              "avg_kernel_us_bracketed": rf["avg_kernel_ms_bracketed"] * 1e3,
-                              "frac_bracketed": rf["frac_bracketed"]},
+           "rocprof_cold_mean_us": statistics.mean(cold), "rocprof_cold_median_us": statistics.median(cold),
+           "rocprof_mall_mean_us": statistics.mean(mall),
+           "frac_rocprof_cold": frac(statistics.mean(cold)), "frac_rocprof_mall": frac(statistics.mean(mall)),
+           "bench_same_run": {"avg_launch_us": rf["avg_launch_ms"] * 1e3, "frac": rf["frac"]},
            "algorithmic_bytes_per_launch": algo}
-    out["bracketed_vs_rocprof_cold"] = out["bench_same_run"]["avg_kernel_us_bracketed"] / out["rocprof_cold_mean_us"]
+    out["bench_event_vs_rocprof_cold"] = out["bench_same_run"]["avg_launch_us"] / out["rocprof_cold_mean_us"]
     print(json.dumps(out, indent=1))
 
 
