@@ -3,7 +3,10 @@
 // dtypes.  Argument checking and error strings live in dpac_abi.hip.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "dpac_mlp_grad.h"
+#include "dpac_mlp_grad_x3.h"
 #include "dpac_mlp_rows.h"
 #include "dpac_mlp_x3.h"
 
@@ -101,21 +104,124 @@ PgFork* pg_fork() {
   return &r;
 }
 
+// one layer of the f32 / f64 kernel (k_param_grads): the wave grid and the tile counts are
+// template bins (wide layers: 1 x 4 waves, 2 column tiles each (f64: 1), row tiles
+// 1/2/4/8/13/16; layers of <= 32 outputs: 4 x 1 waves over the row tiles)
+template <typename T>
+int launch_f32_layer(const PgArgs<T>& a, int l, int64_t nch, hipStream_t s) {
+  const int K = a.width[l], H = a.width[l + 1];
+  const int nti = (K + 15) / 16;
+  if (H <= 32) {
+    const int ntj = (H + 15) / 16, nt4 = (nti + 3) / 4;
+    const dim3 grid((unsigned)nch, 1u);
+#define DPAC_PGN(NI, NJ) hipLaunchKernelGGL((k_param_grads<T, NI, NJ, 4>), grid, dim3(kPgThreads), 0, s, a, l)
+#define DPAC_PGN_J(NI) if (ntj == 1) DPAC_PGN(NI, 1); else DPAC_PGN(NI, 2);
+    if (nt4 <= 1) { DPAC_PGN_J(1) }
+    else if (nt4 <= 2) { DPAC_PGN_J(2) }
+    else if (nt4 <= 3) { DPAC_PGN_J(3) }
+    else { DPAC_PGN_J(4) }
+#undef DPAC_PGN_J
+#undef DPAC_PGN
+  } else {
+    constexpr int NJ = sizeof(T) == 4 ? 2 : 1;
+    constexpr int CW = 16 * NJ * 4;
+    const dim3 grid((unsigned)nch, (unsigned)((H + CW - 1) / CW));
+#define DPAC_PG(NI) hipLaunchKernelGGL((k_param_grads<T, NI, NJ, 1>), grid, dim3(kPgThreads), 0, s, a, l)
+    if (nti <= 1) DPAC_PG(1);
+    else if (nti <= 2) DPAC_PG(2);
+    else if (nti <= 4) DPAC_PG(4);
+    else if (nti <= 8) DPAC_PG(8);
+    else if (nti <= 13) DPAC_PG(13);
+    else DPAC_PG(16);
+#undef DPAC_PG
+  }
+  return (int)hipGetLastError();
+}
+
+// Whether a float network's parameter gradients run on split-fp16 MFMA (dpac_mlp_grad_x3.h):
+// the caller gave the split-fp16 weight images (it asked for split-fp16 products), every
+// width fits the staging map, and DPAC_PG_X3=0 does not force the f32 kernel (tests).
+inline bool pg_x3(const dpac_mlp& net) {
+  const char* e = getenv("DPAC_PG_X3");  // read per launch
+  if (e && e[0] == '0') return false;
+  for (int i = 0; i <= net.n_hidden; ++i)
+    if (!net.weight_x3[i]) return false;
+  for (int i = 0; i <= net.n_hidden + 1; ++i)
+    if (net.width[i] > DPAC_MLP_MAX_WIDTH) return false;
+  return true;
+}
+
+// one layer of the split-fp16 kernel: wide outputs 1 x 8 waves (one column tile each,
+// 128-column groups), outputs of <= 32 columns 8 x 1 waves over the row tiles
+int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
+  const int K = a.width[l], H = a.width[l + 1];
+  const int nti = (K + 15) / 16;
+  if (H <= 32) {
+    const int ntj = (H + 15) / 16, nt8 = (nti + 7) / 8;
+    const dim3 grid((unsigned)nch, 1u);
+#define DPAC_PGX(NI, NJ) hipLaunchKernelGGL((k_param_grads_x3<NI, NJ, 8, false>), grid, dim3(kPgxThreads), 0, s, a, l)
+    if (nt8 <= 1) {
+      if (ntj == 1) DPAC_PGX(1, 1); else DPAC_PGX(1, 2);
+    } else {
+      if (ntj == 1) DPAC_PGX(2, 1); else DPAC_PGX(2, 2);
+    }
+#undef DPAC_PGX
+  } else {
+    const dim3 grid((unsigned)nch, (unsigned)((H + 127) / 128));
+#define DPAC_PGX(NI, L0) hipLaunchKernelGGL((k_param_grads_x3<NI, 1, 1, L0>), grid, dim3(kPgxThreads), 0, s, a, l)
+    if (l == 0) {  // the input layer (d <= 32: launch() sends the others to the f32 kernel)
+      if (nti <= 1) DPAC_PGX(1, true);
+      else DPAC_PGX(2, true);
+    } else if (nti <= 1) DPAC_PGX(1, false);
+    else if (nti <= 2) DPAC_PGX(2, false);
+    else if (nti <= 4) DPAC_PGX(4, false);
+    else if (nti <= 8) DPAC_PGX(8, false);
+    else DPAC_PGX(13, false);
+#undef DPAC_PGX
+  }
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x, int64_t ldx,
            const void* z, const void* G, void* ws, void* out, hipStream_t s0) {
   PgArgs<T> a = pg_args<T>(net, rows, x, ldx, z, G);
   a.rows_per_chunk = pg_chunk_rows<T>(rows, max_ld(a));
+  if constexpr (std::is_same<T, float>::value) {
+    if (pg_x3(net)) {
+      // 32-row sub-chunks: chunks of a multiple of 32 rows, never more chunks than the
+      // workspace (sized for the f32 kernel's 16-row rounding) holds
+      a.rows_per_chunk = std::max<int64_t>((a.rows_per_chunk + kPgxSR - 1) / kPgxSR * kPgxSR, kPgxSR);
+      const int64_t cap = (((int64_t)1 << 31) - 1) / (max_ld(a) * 4) / kPgxSR * kPgxSR;
+      if (a.rows_per_chunk <= cap) {
+        a.part = (float*)ws;
+        const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
+        for (int l = 0; l <= a.L; ++l) {
+          // layers the split kernel does not cover (a wide layer with more than 13 input
+          // tiles; an input layer wider than 32 or into a layer of <= 32) take the f32
+          // kernel on the same chunks and partial layout
+          const int K = a.width[l], H = a.width[l + 1];
+          const bool x3ok = l == 0 ? (K <= 32 && H > 32) : (H <= 32 || K <= 208);
+          int e = 0;
+          if (x3ok) e = launch_x3_layer(a, l, nch, s0);
+          else e = launch_f32_layer<float>(a, l, nch, s0);
+          if (e) return e;
+        }
+        const int64_t n = a.ptot + a.width[a.L + 1];
+        hipLaunchKernelGGL(k_param_grads_reduce<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s0,
+                           a, (int)nch, (float)gamma_scale, (float*)out);
+        return (int)hipGetLastError();
+      }
+      a.rows_per_chunk = pg_chunk_rows<T>(rows, max_ld(a));
+    }
+  }
   a.part = (T*)ws;
   const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
   // narrow layers (K or H <= 32: grids of 256-512 small workgroups) on the forked
   // stream; every layer writes its own partial columns, so the branches share nothing
   PgFork* fk = DPAC_PG_FORK ? pg_fork() : nullptr;
   bool forked = false;
-  // one launch per layer: the wave grid and the tile counts are template bins
-  // (wide layers: 1 x 4 waves, 2 column tiles each (f64: 1), row tiles
-  // 1/2/4/8/13/16; layers of <= 32 outputs: 4 x 1 waves over the row tiles)
-  for (int l = 0; l <= a.L; ++l) {
+  for (int l = 0; l <= a.L; ++l) {  // one launch per layer
     const int K = a.width[l], H = a.width[l + 1];
     hipStream_t s = s0;
     if (fk && (K <= 32 || H <= 32)) {
@@ -126,31 +232,7 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
       }
       s = fk->aux;
     }
-    const int nti = (K + 15) / 16;
-    if (H <= 32) {
-      const int ntj = (H + 15) / 16, nt4 = (nti + 3) / 4;
-      const dim3 grid((unsigned)nch, 1u);
-#define DPAC_PGN(NI, NJ) hipLaunchKernelGGL((k_param_grads<T, NI, NJ, 4>), grid, dim3(kPgThreads), 0, s, a, l)
-#define DPAC_PGN_J(NI) if (ntj == 1) DPAC_PGN(NI, 1); else DPAC_PGN(NI, 2);
-      if (nt4 <= 1) { DPAC_PGN_J(1) }
-      else if (nt4 <= 2) { DPAC_PGN_J(2) }
-      else if (nt4 <= 3) { DPAC_PGN_J(3) }
-      else { DPAC_PGN_J(4) }
-#undef DPAC_PGN_J
-#undef DPAC_PGN
-    } else {
-      constexpr int NJ = sizeof(T) == 4 ? 2 : 1;
-      constexpr int CW = 16 * NJ * 4;
-      const dim3 grid((unsigned)nch, (unsigned)((H + CW - 1) / CW));
-#define DPAC_PG(NI) hipLaunchKernelGGL((k_param_grads<T, NI, NJ, 1>), grid, dim3(kPgThreads), 0, s, a, l)
-      if (nti <= 1) DPAC_PG(1);
-      else if (nti <= 2) DPAC_PG(2);
-      else if (nti <= 4) DPAC_PG(4);
-      else if (nti <= 8) DPAC_PG(8);
-      else if (nti <= 13) DPAC_PG(13);
-      else DPAC_PG(16);
-#undef DPAC_PG
-    }
+    if (int e = launch_f32_layer<T>(a, l, nch, s)) return e;
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
   if (forked) {

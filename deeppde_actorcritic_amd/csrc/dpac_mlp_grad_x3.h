@@ -1,0 +1,328 @@
+// dpac_mlp_grad_x3.h — k_param_grads (dpac_mlp_grad.h) on split-fp16 MFMA, for float
+// networks whose caller asked for split-fp16 products (dpac_mlp.weight_x3 given).
+//
+// The same sums as k_param_grads (the trainable-variable gradients of DeepNN, solver.py:
+// 227-278, as the GradientTape of solver.py:88,95 forms them):
+//   dW_l = Σ_r a_l[r]^T (G_{l+1}[r] ⊙ s_{l+1}),  dbeta_i = Σ_r G_i[r],  dgamma_i = rs Σ_r G_i ⊙ zin_i
+// with the reduction over rows as the MFMA's K dimension: one v_mfma_f32_16x16x32_f16 step
+// covers 32 rows.  Operands are split as in dpac_mlp_x3.h (a = hi + lo 2^-12, three MFMAs
+// hi*hi, hi*lo, lo*hi accumulated in f32), so every product is the f32 product
+// to within the f32 accumulation error; the BN column sums stay plain f32 adds.
+// Gradients are small (O(1/B) and far below it in early steps and inner layers), and a value
+// under fp16's normal range (6.1e-5) keeps only an ABSOLUTE error of ~2^-37 through its lo
+// half, so the B operand (G ⊙ s) carries a per-column power of two: each sub-chunk's column
+// max raises a running exponent E_c, the column is staged times 2^(3 - E_c) (|values| < 8),
+// the lane's accumulator of that column is rescaled by 2^(E_old - E_new) when E_c rises
+// (exact), and the partial is unscaled by 2^(E_c - 3) when written.  (A per-row scale, as the
+// backward chains use, cannot be undone after a reduction over rows.)  With |B| < 8 the three
+// products share ONE accumulator: acc += A_hi (2^12 B_hi) + A_hi B_lo + A_lo B_hi (= 2^12 A B;
+// 2^12 B_hi < 32768 is an exact fp16 number), half the accumulator registers of two chains.
+//
+// Workgroup (chunk c, column group g, layer l) = 8 wavefronts; a sub-chunk of 32 rows is
+// staged through LDS per step:
+//  * staging: thread (rb = tid / 128, f = tid % 128) loads rows 8 rb .. 8 rb + 7 of A feature
+//    f (+128) and of B column f — coalesced dword loads along the row — applies BN and the
+//    activation (A) or the BN scale (B), splits, and writes each 8-row run as ONE 16-byte LDS
+//    write per part: the images are [part][row block][feature][8 rows] halves, which is
+//    exactly the MFMA fragment order (lane l reads feature l & 15, row block l >> 4), so a
+//    fragment read is 4 runs of 256 contiguous bytes;
+//  * MFMA: wave (wi, wj) of a WI x WJ grid owns row tiles wi + WI ti (features of layer l)
+//    and column tiles wj + WJ jj of the group.  Wide layers: WI = 1, WJ = 8, one column tile
+//    per wave (CW = 128 columns, 2 groups at H = 200); outputs of <= 32 columns: WI = 8,
+//    WJ = 1 (the waves split the row tiles).
+// Partials go to the same [chunk][ptot] layout k_param_grads_reduce sums.
+#pragma once
+
+#include "dpac_mlp_grad.h"
+
+namespace dpac {
+
+typedef _Float16 pgh8 __attribute__((ext_vector_type(8)));
+typedef float pgf4 __attribute__((ext_vector_type(4)));
+
+constexpr int kPgxThreads = 512;
+constexpr int kPgxWaves = 8;
+constexpr int kPgxSR = 32;  // rows per sub-chunk = the MFMA's K
+#ifndef DPAC_PGX_DEPTH
+#define DPAC_PGX_DEPTH 1  // register stages of loads in flight (2 measured: no gain, 0.628 vs 0.628 ms at 204 800 rows)
+#endif
+constexpr int kPgxDepth = DPAC_PGX_DEPTH;
+static_assert(kPgxDepth == 1 || kPgxDepth == 2, "1 or 2 stages");
+constexpr float kPgxLo = 4096.f, kPgxLoInv = 1.f / 4096.f;
+
+// staged values of one sub-chunk (registers; loaded before the previous sub-chunk's MFMAs)
+template <int QA, bool L0>
+struct PgxStage {
+  float a[QA][8];             // zin_l at rows 8 rb + i, features f + 128 q
+  float g0[L0 ? QA : 1][8];   // layer 0: G_0 at the same places (BN_0 sums)
+  float gb[8];      // G_{l+1} at column col0 + f
+  float zb[8];      // zin_{l+1} (pre-bias) at the same places
+};
+
+__device__ __forceinline__ void pgx_split8(const float (&v)[8], pgh8& h, pgh8& l) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h[i] = (_Float16)v[i];
+    l[i] = (_Float16)((v[i] - (float)h[i]) * kPgxLo);
+  }
+}
+
+template <int NTI, int NTJ, int WI, bool L0>
+__global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<float> a, const int l) {
+  constexpr int WJ = kPgxWaves / WI;
+  constexpr int CW = 16 * NTJ * WJ;                     // B columns per workgroup (<= 128)
+  constexpr int KP = 16 * NTI * WI;                     // staged A features
+  constexpr int QA = (KP + 127) / 128;                  // A features per staging thread
+  static_assert(CW <= 128 && KP <= DPAC_MLP_MAX_WIDTH, "staging map: 128 columns, 256 features");
+  // LDS: the images, halves A [2 parts][4 row blocks][KP][8], B [3][4][CW][8] (hi, lo,
+  // 2^12 hi); after the
+  // row loop the same bytes hold the BN column sums' reduction ([4 rb][2][128] floats for
+  // the B side, then [4 rb][2][128 QA] for BN_0 on the input layer)
+  constexpr int kImgBytes = (2 * KP + 3 * CW) * 4 * 8 * 2;
+  constexpr int kRedFloats = 4 * 2 * 128 + (L0 ? 4 * 2 * 128 * QA : 0);
+  constexpr int kMain = kImgBytes > kRedFloats * 4 ? kImgBytes : kRedFloats * 4;
+  // then the column scaling: sub-chunk maxima [4 rb][CW], rescale factors [CW], exponents [CW]
+  constexpr int kSmem = kMain + (4 * CW + 2 * CW) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kSmem];
+  _Float16* const sA = reinterpret_cast<_Float16*>(smem);
+  _Float16* const sB = sA + 2 * 4 * KP * 8;
+  float* const s_cmax = reinterpret_cast<float*>(smem + kMain);
+  float* const s_cfac = s_cmax + 4 * CW;
+  int* const s_cexp = reinterpret_cast<int*>(s_cfac + CW);
+  const int grp = blockIdx.y;
+  const int K = a.width[l], H = a.width[l + 1];
+  const int col0 = grp * CW;
+  if (col0 >= H) return;  // whole workgroup, before any barrier
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wave / WJ, wj = wave % WJ;
+  const int rb = tid >> 7, fl = tid & 127;
+  const int64_t chunk = blockIdx.x;
+  const int64_t r_begin = chunk * a.rows_per_chunk;
+  const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
+  const bool first = L0 && grp == 0;  // also sums BN_0 (L0: l == 0)
+  const bool last = l == a.L;             // zin_{L+1} = z_{L+1} + bias
+  const float* srcA = l == 0 ? a.x : a.z + a.zoff[l];
+  const int64_t ldA = l == 0 ? a.ldx : a.ztot;
+  const float* gA = a.G + a.goff[0];
+  const float* gB = a.G + a.goff[l + 1] + col0;
+  const float* zB = a.z + a.zoff[l + 1] + col0;
+
+  // per-thread constants: A features fl + 128 q, B column col0 + fl
+  float sa[QA], ha[QA];
+  uint32_t offA[QA], offG0[QA];
+#pragma unroll
+  for (int q = 0; q < QA; ++q) {
+    const int k = fl + 128 * q;
+    const bool v = k < K;
+    sa[q] = v ? a.scale[l][k] : 0.f;
+    ha[q] = v ? a.shift[l][k] : 0.f;
+    offA[q] = v ? (uint32_t)k * 4u : kOOB;
+    offG0[q] = (v && first) ? (uint32_t)k * 4u : kOOB;
+  }
+  const int hcol = col0 + fl;
+  const bool bv = fl < CW && hcol < H;
+  const float sbv = bv ? a.scale[l + 1][hcol] : 0.f;
+  const float bbv = (bv && last) ? a.bias[hcol] : 0.f;
+  const uint32_t offB = bv ? (uint32_t)fl * 4u : kOOB;
+  float cs0_b[QA], cs0_s[QA], csb_b = 0.f, csb_s = 0.f;
+  int cexp = -100;  // the column's running exponent (B staging threads)
+#pragma unroll
+  for (int q = 0; q < QA; ++q) cs0_b[q] = cs0_s[q] = 0.f;
+  pgf4 acc[NTI][NTJ];  // 2^12 x (the column-scaled) dW tile
+#pragma unroll
+  for (int ti = 0; ti < NTI; ++ti)
+#pragma unroll
+    for (int jj = 0; jj < NTJ; ++jj) acc[ti][jj] = pgf4{0.f, 0.f, 0.f, 0.f};
+
+  // loads of the 32 rows at r0: descriptors based at row r0 ending at the chunk's last row
+  // (rows past it read 0, so their G is 0 and they add nothing); masked columns carry kOOB
+  auto issue = [&](int64_t r0, PgxStage<QA, L0>& st) {
+    const int64_t nr = r_end - r0;  // >= 1
+    const auto rA = make_rsrc(srcA + r0 * ldA, (uint32_t)(((nr - 1) * ldA + K) * 4));
+    const auto rG = make_rsrc(gA + r0 * a.gtot, (uint32_t)(((nr - 1) * a.gtot + K) * 4));
+    const auto rB = make_rsrc(gB + r0 * a.gtot, (uint32_t)(((nr - 1) * a.gtot + (H - col0)) * 4));
+    const auto rZ = make_rsrc(zB + r0 * a.ztot, (uint32_t)(((nr - 1) * a.ztot + (H - col0)) * 4));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t r = (uint32_t)(8 * rb + i);
+#pragma unroll
+      for (int q = 0; q < QA; ++q) {
+        st.a[q][i] = buf_load_elem<float>(rA, offA[q] + r * (uint32_t)ldA * 4u);
+        if constexpr (L0) st.g0[q][i] = first ? buf_load_elem<float>(rG, offG0[q] + r * (uint32_t)a.gtot * 4u) : 0.f;
+      }
+      st.gb[i] = buf_load_elem<float>(rB, offB + r * (uint32_t)a.gtot * 4u);
+      st.zb[i] = buf_load_elem<float>(rZ, offB + r * (uint32_t)a.ztot * 4u);
+    }
+  };
+
+  const int fq = lane >> 4, fi = lane & 15;  // fragment: row block, feature / column in the tile
+  // one sub-chunk of 32 rows from its staged registers `st`, which are then refilled with
+  // the sub-chunk kPgxDepth ahead (kPgxDepth register stages in flight)
+  auto sub = [&](int64_t r0, PgxStage<QA, L0>& st) {
+    __syncthreads();  // the previous sub-chunk's fragment reads are done
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int k = fl + 128 * q;
+      if (k >= KP) continue;  // compile-time for q = 0 when KP >= 128
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float zi = st.a[q][i];
+        const float y = ha[q] + zi * sa[q];  // the forward's expression (FwdEpi / write_a0)
+        v[i] = k < K ? (l == 0 ? y : y + fmaxf(y, 0.f)) : 0.f;  // rows past the end: a = shift,
+        if constexpr (L0) {                                       // masked by G = 0
+          cs0_b[q] += st.g0[q][i];
+          cs0_s[q] += st.g0[q][i] * zi;
+        }
+      }
+      pgh8 h, lo;
+      pgx_split8(v, h, lo);
+      *reinterpret_cast<pgh8*>(sA + ((0 * 4 + rb) * KP + k) * 8) = h;
+      *reinterpret_cast<pgh8*>(sA + ((1 * 4 + rb) * KP + k) * 8) = lo;
+    }
+    float vb[8];
+    if (fl < CW) {
+      float m = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float gv = st.gb[i];
+        vb[i] = gv * sbv;
+        m = fmaxf(m, fabsf(vb[i]));
+        csb_b += gv;
+        csb_s += gv * (st.zb[i] + bbv);  // bbv = 0 unless the output layer
+      }
+      s_cmax[rb * CW + fl] = m;
+    }
+    __syncthreads();  // the column maxima of the sub-chunk
+    if (fl < CW) {
+      const float m = fmaxf(fmaxf(s_cmax[fl], s_cmax[CW + fl]), fmaxf(s_cmax[2 * CW + fl], s_cmax[3 * CW + fl]));
+      int e = cexp;
+      if (m > 0.f && m < 3.0e38f) {
+        int em = 0;
+        (void)frexpf(m, &em);  // m in [2^(em-1), 2^em)
+        e = em > cexp ? em : cexp;
+      }
+      const float sc = ldexpf(1.f, 3 - e);  // the column's values times sc: |v| < 8
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vb[i] *= sc;
+      pgh8 h, lo, h12;
+      pgx_split8(vb, h, lo);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) h12[i] = h[i] * (_Float16)kPgxLo;  // exact: |h| < 8
+      *reinterpret_cast<pgh8*>(sB + ((0 * 4 + rb) * CW + fl) * 8) = h;
+      *reinterpret_cast<pgh8*>(sB + ((1 * 4 + rb) * CW + fl) * 8) = lo;
+      *reinterpret_cast<pgh8*>(sB + ((2 * 4 + rb) * CW + fl) * 8) = h12;
+      if (rb == 0) {
+        s_cfac[fl] = ldexpf(1.f, cexp - e);  // the accumulated column, to the new scale (exact)
+        s_cexp[fl] = e;
+      }
+      cexp = e;
+    }
+    __syncthreads();
+    if (r0 + kPgxDepth * kPgxSR < r_end) issue(r0 + kPgxDepth * kPgxSR, st);  // lands kPgxDepth sub-chunks later
+    pgh8 bh[NTJ], bl[NTJ], b12[NTJ];
+#pragma unroll
+    for (int jj = 0; jj < NTJ; ++jj) {
+      const int c = (wj + WJ * jj) * 16 + fi;
+      bh[jj] = *reinterpret_cast<const pgh8*>(sB + ((0 * 4 + fq) * CW + c) * 8);
+      bl[jj] = *reinterpret_cast<const pgh8*>(sB + ((1 * 4 + fq) * CW + c) * 8);
+      b12[jj] = *reinterpret_cast<const pgh8*>(sB + ((2 * 4 + fq) * CW + c) * 8);
+      const float f = s_cfac[c];
+      if (__any(f != 1.f)) {  // a column's exponent rose: rescale what it accumulated
+#pragma unroll
+        for (int ti = 0; ti < NTI; ++ti) acc[ti][jj] *= f;
+      }
+    }
+    auto fragA = [&](int ti, int part) {
+      const int k = (wi + WI * ti) * 16 + fi;
+      return *reinterpret_cast<const pgh8*>(sA + ((part * 4 + fq) * KP + k) * 8);
+    };
+    pgh8 xh = fragA(0, 0), xl = fragA(0, 1);
+#pragma unroll
+    for (int ti = 0; ti < NTI; ++ti) {  // A fragments one tile ahead (pinned: not all hoisted)
+      pgh8 nh = xh, nl = xl;
+      if (ti + 1 < NTI) {
+        nh = fragA(ti + 1, 0);
+        nl = fragA(ti + 1, 1);
+      }
+#pragma unroll
+      for (int jj = 0; jj < NTJ; ++jj) {
+        acc[ti][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, b12[jj], acc[ti][jj], 0, 0, 0);
+        acc[ti][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, bl[jj], acc[ti][jj], 0, 0, 0);
+        acc[ti][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, bh[jj], acc[ti][jj], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      xh = nh;
+      xl = nl;
+    }
+  };
+  PgxStage<QA, L0> st0;
+  issue(r_begin, st0);
+  if constexpr (kPgxDepth == 1) {
+    for (int64_t r0 = r_begin; r0 < r_end; r0 += kPgxSR) sub(r0, st0);
+  } else {
+    PgxStage<QA, L0> st1;
+    if (r_begin + kPgxSR < r_end) issue(r_begin + kPgxSR, st1);
+    for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * kPgxSR) {
+      sub(r0, st0);
+      if (r0 + kPgxSR < r_end) sub(r0 + kPgxSR, st1);
+    }
+  }
+
+  // ---- this chunk's partial dW_l: lane holds features 4 fq .. +3 of its row tile, column fi ----
+  float* part = a.part + chunk * a.ptot;
+#pragma unroll
+  for (int ti = 0; ti < NTI; ++ti) {
+#pragma unroll
+    for (int jj = 0; jj < NTJ; ++jj) {
+      const int h = col0 + (wj + WJ * jj) * 16 + fi;
+      // undo 2^12 and the column scale 2^(3 - E_c)
+      const float us = ldexpf(1.f, s_cexp[(wj + WJ * jj) * 16 + fi] - 3 - 12);
+      const pgf4 c = acc[ti][jj] * us;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int k = (wi + WI * ti) * 16 + 4 * fq + v;
+        if (k < K && h < H) part[a.off_W[l] + (int64_t)k * H + h] = c[v];
+      }
+    }
+  }
+  // ---- BN column sums: combine the 4 row blocks through LDS (reusing the images) ----
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  float* red0 = red + 4 * 2 * 128;
+  red[(rb * 2 + 0) * 128 + fl] = csb_b;
+  red[(rb * 2 + 1) * 128 + fl] = csb_s;
+  if constexpr (L0) {
+    if (first) {
+#pragma unroll
+      for (int q = 0; q < QA; ++q) {
+        red0[(rb * 2 + 0) * 128 * QA + fl + 128 * q] = cs0_b[q];
+        red0[(rb * 2 + 1) * 128 * QA + fl + 128 * q] = cs0_s[q];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < CW && col0 + tid < H) {
+    float sb = 0.f, ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sb += red[(w * 2 + 0) * 128 + tid];
+      ss += red[(w * 2 + 1) * 128 + tid];
+    }
+    part[a.off_beta[l + 1] + col0 + tid] = sb;
+    part[a.off_gamma[l + 1] + col0 + tid] = ss;
+  }
+  if (L0 && first && tid < K && tid < 128 * QA) {
+    float sb = 0.f, ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sb += red0[(w * 2 + 0) * 128 * QA + tid];
+      ss += red0[(w * 2 + 1) * 128 * QA + tid];
+    }
+    part[a.off_beta[0] + tid] = sb;
+    part[a.off_gamma[0] + tid] = ss;
+  }
+}
+
+}  // namespace dpac

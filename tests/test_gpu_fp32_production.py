@@ -5,7 +5,7 @@ The production float32 path differs from the float64 one in code, not only in pr
   * the actor-shape fast path of the fused rollout / BPTT (16-row tiles, taken for B > 1024 and
     193..208-wide hidden layers), whose products run on split-fp16 MFMA (dpac_rollout_nn_x3.h:
     three v_mfma_f32_16x16x32_f16 per 32-k step, f32 accumulate), as do the critic's V / G row
-    kernels (dpac_mlp_x3.h);
+    kernels (dpac_mlp_x3.h) and every network's parameter gradients (dpac_mlp_grad_x3.h);
   * the BPTT reading the forward's activation sign bits (dpac_rollout_nn_*_masked);
   * the k-major weight images (dwordx4 B loads);
   * the critic's G network with the TD1 dot fused (dpac_mlp_rows_fwd_td1), HIP graphs and the
@@ -56,7 +56,7 @@ TOL_PARAM = 2e-4     # parameter summaries, |a - b| <= TOL_PARAM (1 + |b|)
 def _default_paths(monkeypatch):
     """The production selection: no test override of the kernel choice."""
     for k in ("DPAC_NN_TILE", "DPAC_NN_FAST", "DPAC_NN_X3", "DPAC_BPTT", "DPAC_MASK_BPTT", "DPAC_WEIGHT_KM",
-              "DPAC_MLP_MATH"):
+              "DPAC_MLP_MATH", "DPAC_PG_X3"):
         monkeypatch.delenv(k, raising=False)
     assert ops.MASK_BPTT and ops.WEIGHT_KM == "on" and ops.CRITIC_TD1 == "fused"
     assert ops.BPTT_MODE == "fused" and ops.ROW_MLP == "kernel" and ops.PARAM_GRADS == "kernel"

@@ -83,6 +83,52 @@ def test_param_grads_vs_torch(widths, R, dtype):
         assert err <= tol, (a.shape, err)
 
 
+@pytest.mark.parametrize("widths,R", [
+    ((20, 200, 200, 200, 20), 20000),      # the lqr_d20 networks, many chunks
+    ((20, 200, 200, 200, 21), 777),        # Eikonal actor head, ragged rows
+    ((5, 256, 256, 256, 256, 1), 3001),    # 16-tile inputs: those layers take the f32 kernel
+    ((4, 7, 2), 1),                        # one row; the input layer into 7 takes the f32 kernel
+    ((10, 48, 130, 33, 10), 4099),         # widths that split MFMA tiles and column groups
+    ((20, 200, 200, 200, 20), 204800)])    # the lqr_d20 critic G network's N*B rows
+@pytest.mark.parametrize("gscale", [1.0, 1e-6, "ramp"])
+def test_param_grads_split_fp16_vs_torch(widths, R, gscale, monkeypatch):
+    """The split-fp16 parameter-gradient kernel (dpac_mlp_grad_x3.h, selected by a view that
+    carries weight_x3 images) against the float64 sums and the exact-f32 kernel on the same
+    inputs, per tensor within 2e-5 of its largest entry (the f32 kernel's bound) and within
+    4x the f32 kernel's error + 2e-6: for O(1) gradients, for gradients of 1e-6 scale (fp16-
+    subnormal without the kernel's per-column scale) and for a ramp over rows from 1e-9 to 1
+    (each column's running exponent rises sub-chunk after sub-chunk: accumulator rescaling)."""
+    if R == 204800 and gscale != 1.0:
+        pytest.skip("one scale at full size")
+    scales, shifts, Ws, b = random_net(widths, torch.float32, seed=len(widths) + R)
+    g = torch.Generator().manual_seed(R)
+    rnd = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(torch.float32).to(DEV)
+    x = rnd(R, widths[0])
+    z = rnd(R, sum(widths[1:]))
+    G = rnd(R, sum(widths))
+    if gscale == "ramp":
+        G = G * torch.logspace(-9, 0, R, dtype=torch.float64).to(torch.float32).to(DEV).unsqueeze(1)
+    else:
+        G = G * gscale
+    view = ops.MlpView(scales, shifts, Ws, b, False, weights_x3=[_x3_image(W) for W in Ws])
+    like = scales + shifts + Ws + [b]
+    rs = ops.bn_rs_host(torch.float32)
+    monkeypatch.delenv("DPAC_PG_X3", raising=False)
+    got = ops.mlp_param_grads(view, x, z, G, like)
+    monkeypatch.setenv("DPAC_PG_X3", "0")
+    f32 = ops.mlp_param_grads(view, x, z, G, like)
+    ref = reference_grads(widths, scales, shifts, Ws, b, rs, x, z, G)
+    worst = 0.0
+    for a, a32, r in zip(got, f32, ref):
+        assert a.shape == r.shape
+        top = float(r.abs().max())
+        err = float((a.double() - r).abs().max()) / (top + 1e-300)
+        err32 = float((a32.double() - r).abs().max()) / (top + 1e-300)
+        worst = max(worst, err)
+        assert err <= 2e-5 and err <= 4 * err32 + 2e-6, (a.shape, err, err32)
+    print(f"\n[x3 param grads {widths} R={R} G~{gscale}] max rel err {worst:.2e}")
+
+
 def test_param_grads_strided_input_and_bad_args():
     widths = (20, 64, 20)
     scales, shifts, Ws, b = random_net(widths, torch.float64, seed=5)

@@ -15,7 +15,7 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_train/run_kernel_t
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 # the last iteration: from the first kernel after the Adam step that precedes its two
 # forward rollouts (its samples were drawn at the end of the previous iteration)
-fwd = [i for i, r in enumerate(rows) if re.search(r"k_rollout_nn4?<", r["Kernel_Name"])]
+fwd = [i for i, r in enumerate(rows) if re.search(r"k_rollout_nn(4|_x3)?<", r["Kernel_Name"])]
 t_first = int(rows[fwd[-2]]["Start_Timestamp"])
 adam = [i for i, r in enumerate(rows) if "k_adam" in r["Kernel_Name"] and int(r["End_Timestamp"]) <= t_first]
 a = adam[-1] + 1 if adam else fwd[-2]
