@@ -175,8 +175,9 @@ def ops_mlp_math(dtype):
     if dtype != torch.float32:
         return "f64 MFMA (v_mfma_f64_16x16x4_f64)"
     if ops.MLP_MATH == "x3":
-        return ("f32 via split-fp16 MFMA in the row-parallel critic kernels (3 v_mfma_f32_16x16x32_f16 "
-                "per product, f32 accumulate; f32-accurate, DESIGN.md 4.3), exact f32 MFMA elsewhere")
+        return ("f32 via split-fp16 MFMA (3 v_mfma_f32_16x16x32_f16 per product, f32 accumulate; "
+                "f32-accurate, DESIGN.md 4.3) in the fused actor rollout / BPTT, the critic's row "
+                "kernels and the parameter gradients")
     return "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
 
 
@@ -341,7 +342,7 @@ def main():
                      "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": per_launch_ms,
                      "note": "achieved = algorithmic bytes / (HIP event pair over the K timed launches / K) on "
                              "the launch stream; rocprofv3's mean duration of the same cold launches agrees "
-                             "within 1% (tools/rocprof_headline.py -> profiles/r03_rocprof_headline.json)"},
+                             "(tools/rocprof_headline.py -> profiles/r03_rocprof_headline.json, cold launches only)"},
     }
     if not args.no_variants:
         progress("variants: MALL-resident, in-kernel Philox, float64, TD1, fused NN rollout")

@@ -9,6 +9,7 @@
   gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream -> x2)
 * profiles/pmc_traffic.json        — the per-launch HBM bytes bench.py reports as
   roofline.traffic for the matching workload key
+* profiles/<tag>_rocprof_headline.json, <tag>_pmc_mlp.json, <tag>_train_timeline.txt
 """
 import csv
 import json
@@ -42,6 +43,14 @@ def main(tag):
                             capture_output=True, text=True)
         if tl.returncode == 0:
             open(os.path.join(PROF, f"{tag}_train_timeline.txt"), "w").write(tl.stdout)
+    hl = os.path.join(OUT, "headline.log")  # tools/rocprof_headline.py over prof_kt
+    if os.path.exists(hl):
+        txt = open(hl).read()
+        if txt.lstrip().startswith("{"):
+            open(os.path.join(PROF, f"{tag}_rocprof_headline.json"), "w").write(txt)
+    pm = os.path.join(OUT, "pmc_mlp", "summary.json")  # tools/pmc_mlp.sh
+    if os.path.exists(pm):
+        shutil.copy(pm, os.path.join(PROF, f"{tag}_pmc_mlp.json"))
     bl = os.path.join(OUT, "bench.log")
     if os.path.exists(bl):
         lines = [l for l in open(bl) if l.startswith("{")]

@@ -1,7 +1,9 @@
 #!/usr/bin/env bash
 # One round's GPU evidence: GPU tests, smoke(), bench line, rocprofv3 kernel trace of the
-# bench and of the lqr_d20 training iteration, and the two HBM counter passes (FETCH_SIZE,
-# WRITE_SIZE in separate runs, as MI355X_MICROARCH.md §HBM prescribes).  On the GPU box:
+# bench (-> the headline's cold / MALL-resident launch split, tools/rocprof_headline.py) and
+# of the lqr_d20 training iteration, the two HBM counter passes (FETCH_SIZE, WRITE_SIZE in
+# separate runs, as MI355X_MICROARCH.md §HBM prescribes), and the MLP kernels' counters
+# (tools/pmc_mlp.sh).  On the GPU box:
 #   gpurun -- 'bash tools/profile_round.sh'   then   python tools/collect_profiles.py rNN
 source tools/gpu_steps.sh
 export TMPDIR=/tmp
@@ -10,8 +12,10 @@ rm -f gpurun_out/steps.log
 rm -rf gpurun_out/prof_kt gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof_train
 run 900 pytest_gpu python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread
 run 300 smoke python -u -c "import __graft_entry__ as g; g.smoke()"
-run 300 bench python bench.py --steps 200 --warmup 20
+run 400 bench python -u bench.py --steps 200 --warmup 20
 run 300 prof_kt rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-train
+run 60 headline python tools/rocprof_headline.py gpurun_out/prof_kt/run_kernel_trace.csv gpurun_out/prof_kt.log --steps 100 --warmup 10
 run 300 prof_train rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_train -o run --output-format csv -- python tools/train_bench.py --iters 3 --warmup 1 --dtype float32
 run 300 pmc_fetch rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
 run 300 pmc_write rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
+run 900 pmc_mlp bash tools/pmc_mlp.sh
