@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPAC_LIB", os.path.join(_HERE, "libdpac.so"))
 
 # constants mirrored from include/dpac.h
-ABI_VERSION = 4  # DPAC_ABI_VERSION: load() refuses a library built from another header
+ABI_VERSION = 5  # DPAC_ABI_VERSION: load() refuses a library built from another header
 DPAC_OK, DPAC_EINVAL, DPAC_EUNSUP = 0, -1, -2
 F32, F64 = 0, 1
 EQN_LQR, EQN_VDP, EQN_EKN, EQN_LQR_VAR = 0, 1, 2, 3
@@ -114,6 +114,7 @@ SIGNATURES = {
     "dpac_mlp_param_grads": [_I32, _I64, ctypes.POINTER(Mlp), _D, _P, _I64, _P, _P, _P, _I64, _P,
                              _P],
     "dpac_mlp_prepare": [_I32, ctypes.POINTER(Mlp), _D, _P, _P, _P, _P, _P, _P, _P],
+    "dpac_critic_loss_grad": [_I32, _I64, _P, _P, _P, _P, _D, _D, _P, _P, _P],
     "dpac_adam_apply": [_I32, _I32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_void_p),
                         ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                         ctypes.POINTER(ctypes.c_void_p), _D, _D, _D, _D, _P],

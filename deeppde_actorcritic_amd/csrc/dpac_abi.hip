@@ -30,6 +30,8 @@ int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void
                         hipStream_t s);
 int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
                        void* wkm, void* wtkm, void* wx3, void* wtx3, hipStream_t s);
+int critic_loss_launch(int dtype, int64_t B, const void* V, const void* y, const void* disc, const void* zb,
+                       double scale, double clip, void* g_out, void* neg_g, hipStream_t s);
 int adam_launch(int dtype, int n, const int64_t* numel, void* const* var, const void* const* grad,
                 void* const* m, void* const* v, double alpha, double b1, double b2, double eps,
                 hipStream_t s);
@@ -803,6 +805,24 @@ int dpac_adam_apply(int32_t dtype, int32_t n_tensors, const int64_t* numel, void
   }
   const int r = adam_launch(dtype, n_tensors, numel, var, grad, m, v, alpha, beta_1, beta_2,
                             epsilon, (hipStream_t)stream);
+  if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
+  return ok();
+}
+
+int dpac_critic_loss_grad(int32_t dtype, int64_t num_sample, const void* V, const void* y, const void* disc,
+                          const void* z_bdry, double scale, double delta_clip, void* g_out, void* neg_g,
+                          void* stream) {
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
+  if (num_sample < 1) return fail(DPAC_EINVAL, "num_sample must be >= 1 (got %lld)", (long long)num_sample);
+  if (!(delta_clip > 0)) return fail(DPAC_EINVAL, "delta_clip must be > 0");
+  DPAC_REQUIRE(V);
+  DPAC_REQUIRE(y);
+  DPAC_REQUIRE(disc);
+  DPAC_REQUIRE(z_bdry);
+  DPAC_REQUIRE(g_out);
+  DPAC_REQUIRE(neg_g);
+  const int r = critic_loss_launch(dtype, num_sample, V, y, disc, z_bdry, scale, delta_clip, g_out, neg_g,
+                                   (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();
 }

@@ -1,6 +1,7 @@
 // dpac_params.hip — kernels on the parameters of the MLPs rather than on
 // trajectories: the derived tensors every MLP kernel reads (dpac_mlp_prepare) and
-// the optimizer step (dpac_adam_apply).
+// the optimizer step (dpac_adam_apply); and the critic loss's gradient at V's output
+// (dpac_critic_loss_grad), the one elementwise step between the critic's kernels.
 //
 // Adam: one optimizer step of TF-form Adam over a list of parameter tensors in
 // one launch (the reference's tf.keras Adam, solver.py:16-21, whose
@@ -230,6 +231,47 @@ int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, void* km
 }
 
 }  // namespace
+
+// dpac_critic_loss_grad: the gradient of loss_critic (solver.py:73-78) at V's outputs, from
+// V at [x_0; x_N; x_bdry] (3B), the TD target y, the discount disc_N and Z_tf(x_bdry)
+// (solver.py:189-190):
+//   delta = (V0 - y) - VN * disc,  delta_b = Vb - zb,
+//   h'(z) = 2 z if |z| < clip else (2 clip) sign(z),   g = h'(delta) * scale,  g_b = h'(delta_b) * scale,
+//   g_out = [g; (-g) * disc; g_b],  neg_g = -g   (dL/dy, what the TD backward reads)
+// each operation rounded as the same tensor expressions round them (-ffp-contract=off).
+template <typename T>
+__global__ __launch_bounds__(256) void k_critic_loss_grad(int64_t B, const T* __restrict__ V, const T* __restrict__ y,
+                                                          const T* __restrict__ disc, const T* __restrict__ zb,
+                                                          T scale, T clip, T* __restrict__ g_out,
+                                                          T* __restrict__ neg_g) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  auto hgrad = [&](T z) {
+    const T sg = z > T(0) ? T(1) : (z < T(0) ? T(-1) : z);  // sign(z); NaN stays NaN as in torch.where
+    return fabs(z) < clip ? T(2) * z : (T(2) * clip) * sg;
+  };
+  const T dc = disc[b];
+  const T delta = (V[b] - y[b]) - V[B + b] * dc;
+  const T delta_b = V[2 * B + b] - zb[b];
+  const T g = hgrad(delta) * scale;
+  g_out[b] = g;
+  g_out[B + b] = (-g) * dc;
+  g_out[2 * B + b] = hgrad(delta_b) * scale;
+  neg_g[b] = -g;
+}
+
+int critic_loss_launch(int dtype, int64_t B, const void* V, const void* y, const void* disc, const void* zb,
+                       double scale, double clip, void* g_out, void* neg_g, hipStream_t s) {
+  const dim3 grid((unsigned)((B + 255) / 256));
+  if (dtype == DPAC_F64)
+    hipLaunchKernelGGL(k_critic_loss_grad<double>, grid, dim3(256), 0, s, B, (const double*)V, (const double*)y,
+                       (const double*)disc, (const double*)zb, scale, clip, (double*)g_out, (double*)neg_g);
+  else
+    hipLaunchKernelGGL(k_critic_loss_grad<float>, grid, dim3(256), 0, s, B, (const float*)V, (const float*)y,
+                       (const float*)disc, (const float*)zb, (float)scale, (float)clip, (float*)g_out,
+                       (float*)neg_g);
+  return (int)hipGetLastError();
+}
 
 int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
                        void* km, void* tkm, void* x3, void* tx3, hipStream_t s) {

@@ -608,6 +608,21 @@ def td_assemble_gdot(eqp, x, u, dt, coef, gdot, *, cost_order: int = _lib.COST_C
     return y, disc
 
 
+def critic_loss_grad(V, y, disc, z_bdry, scale: float, delta_clip: float):
+    """dpac_critic_loss_grad: (g_out [3B, 1], -g [B]) — loss_critic's gradient at
+    V = NN_value([x_0; x_N; x_bdry]) (solver.py:73-78, 189-190), one launch."""
+    _require_gpu(V, y, disc, z_bdry)
+    B = y.shape[0]
+    V, y, disc, z_bdry = V.contiguous(), y.contiguous(), disc.contiguous(), z_bdry.contiguous()
+    if V.numel() != 3 * B or disc.numel() != B or z_bdry.numel() != B:
+        raise ValueError("critic_loss_grad: V needs 3B entries, disc and z_bdry B")
+    g_out = torch.empty(3 * B, 1, dtype=y.dtype, device=y.device)
+    neg_g = torch.empty(B, dtype=y.dtype, device=y.device)
+    call("dpac_critic_loss_grad", _dtype_id(y), B, _ptr(V), _ptr(y), _ptr(disc), _ptr(z_bdry),
+         float(scale), float(delta_clip), _ptr(g_out), _ptr(neg_g), _stream(y))
+    return g_out, neg_g
+
+
 def td_assemble_bwd_gdot(eqp, dt, coef, g_y):
     """d L / d gdot [N, B] = −g_y·disc_t·coef_t·√dt_t given dL/dy [B]."""
     _require_gpu(dt, coef, g_y)

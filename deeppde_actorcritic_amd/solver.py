@@ -18,6 +18,7 @@ Both give the same values and gradients.
 from __future__ import annotations
 
 import logging
+import os
 import time
 
 import numpy as np
@@ -362,40 +363,56 @@ class _SplitActorGraphs:
 
 
 class _SplitCriticGraphs:
-    """The critic step as two HIP graphs, split at the G network's output: the front
-    (rollout, G forward with saves, TD assembly, V, the loss and its gradients for
-    V's variables and for G's output) and the G network's backward (input-gradient
-    chain + parameter gradients).  The back graph runs on a side stream beside the
-    actor's BPTT, which needs the updated V only (solver.py:221), not G."""
+    """The critic step as three HIP graphs, split at the G network's output: the head
+    (rollout, G forward with saves, TD assembly, V forward, the loss's gradient at V's
+    output and at G's TD1 dots), V's backward (its parameter gradients), and the G
+    network's backward (input-gradient chain + parameter gradients).  The G backward reads
+    only the head's outputs, so it is launched on a side stream as soon as the head is done:
+    it runs beside V's backward, V's Adam step and the actor's terminal V(x_N) (a chain of
+    small kernels that leaves most CUs idle) and then beside the actor's BPTT, which needs
+    the updated V only (solver.py:221), not G."""
 
-    def __init__(self, front_fn, back_fn, batch: TrajectoryBatch, side):
+    def __init__(self, head_fn, v_fn, back_fn, batch: TrajectoryBatch, side):
         self.static = TrajectoryBatch(*[t.clone() for t in batch])
         self.side = side
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up outside the capture (allocator, autograd)
             for _ in range(2):
-                back_fn(front_fn(self.static))
+                h = head_fn(self.static)
+                v_fn(h[0])
+                back_fn((None,) + tuple(h[1]))
         torch.cuda.current_stream().wait_stream(side)
-        self.g_front, self.g_back = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_front):
-            self.front_out = front_fn(self.static)
+        self.g_head, self.g_v, self.g_back = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_head):
+            self.head_out = head_fn(self.static)
+        with torch.cuda.graph(self.g_v):
+            self.v_out = v_fn(self.head_out[0])
         with torch.cuda.graph(self.g_back):
-            self.back_out = back_fn(self.front_out)
+            self.back_out = back_fn((None,) + tuple(self.head_out[1]))
 
-    def front(self, batch: TrajectoryBatch):
-        """Gradients of V's variables (current stream)."""
+    def head(self, batch: TrajectoryBatch):
+        """The head graph on the current stream."""
         for dst, src in zip(self.static, batch):
             dst.copy_(src)
-        self.g_front.replay()
-        return list(self.front_out[0])
+        self.g_head.replay()
+
+    def grads_v(self):
+        """V's parameter gradients (current stream, after head())."""
+        self.g_v.replay()
+        return list(self.v_out)
 
     def launch_back(self, after: torch.cuda.Event):
         """G's parameter gradients, replayed on the side stream once `after` (recorded
-        behind front()) has passed; use them on the side stream."""
+        behind head()) has passed; use them on the side stream."""
         self.side.wait_event(after)
         with torch.cuda.stream(self.side):
             self.g_back.replay()
         return list(self.back_out)
+
+
+# DPAC_GBACK=early (default): the critic's G backward starts right after the critic head;
+# "late": after V's update and the actor's BPTT are queued (round-2 order; measurement).
+GBACK = os.environ.get("DPAC_GBACK", "early")
 
 
 def _huber_grad(delta):
@@ -625,13 +642,19 @@ class ActorCriticSolver(object):
                 and mc.NN_value_grad.fused_ok() and not mc.NN_value_grad.ekn_head)
 
     def critic_front(self, data):
-        """grad_critic split at the G network, without autograd: the rollout, G =
-        NN_value_grad(x_t) over the N*B rows with saves (solver.py:179), the TD1 target
-        (solver.py:166-187), V at (x_0, x_N, x_bdry) with saves, then the loss
-        100*(mean h(delta) + mean h(delta_bdry)) (solver.py:73-78, 189-190)
-        differentiated by hand: h'(z) = 2z inside |z| < 50, 100 sign(z) outside;
+        """grad_critic split at the G network, without autograd (critic_head + critic_grads_v).
+        Returns (gradients of V's variables, then the G backward's inputs: dL/d(TD1 dot)
+        [N*B] (fused) or dL/dG [N*B, d], G's input rows, G's saves[, u rows, dw rows])."""
+        vstate, back = self.critic_head(data)
+        return (self.critic_grads_v(vstate), *back)
+
+    def critic_head(self, data):
+        """The rollout, G = NN_value_grad(x_t) over the N*B rows with saves (solver.py:179),
+        the TD1 target (solver.py:166-187), V at (x_0, x_N, x_bdry) with saves, then the loss
+        100*(mean h(delta) + mean h(delta_bdry)) (solver.py:73-78, 189-190) differentiated by
+        hand at V's output and at G: h'(z) = 2z inside |z| < 50, 100 sign(z) outside;
         dL/dV(x_0) = g, dL/dV(x_N) = -g*disc, dL/dy = -g, dL/dV(x_bdry) = g_bdry.
-        Returns (gradients of V's variables, dL/dG [N*B, d], G's input rows, G's saves)."""
+        Returns ((V's rows, V's saves, dL/dV), the G backward's inputs)."""
         mc, ec = self.model_critic, self.eqn_config
         d = Equation.to_native(data, self.dtype)
         N, T = ec.num_time_interval_critic, ec.total_time_critic
@@ -654,19 +677,25 @@ class ActorCriticSolver(object):
                                           cost_order=_lib.COST_CRITIC)
             xv = torch.cat([x[0], x[N], d.x_bdry])
             Vout, zV = ops.mlp_rows(Vnet.mlp_view(), xv, save=True)
-            V = Vout[:, 0]
-            delta = V[:B] - y - V[B:2 * B] * disc                      # solver.py:189
-            delta_b = V[2 * B:] - self.bsde.Z_tf(d.x_bdry)[:, 0]       # solver.py:190
-            g = _huber_grad(delta) * (100.0 / B)
-            g_b = _huber_grad(delta_b) * (100.0 / B)
-            g_out = torch.cat([g, -g * disc, g_b]).unsqueeze(1)
+            # delta = V(x_0) - y - V(x_N) disc, delta_b = V(x_bdry) - Z_tf(x_bdry)
+            # (solver.py:189-190) and the Huber gradient, one launch
+            g_out, neg_g = ops.critic_loss_grad(Vout, y, disc, self.bsde.Z_tf(d.x_bdry), 100.0 / B, DELTA_CLIP)
+            if fused:
+                g_gdot = ops.td_assemble_bwd_gdot(eqp, dt, coef, neg_g)
+                back = (g_gdot.reshape(N * B), rows, zG, u_rows, dw_rows)
+            else:
+                gG = ops.td_assemble_bwd(eqp, x, u, d.dw, dt, coef, neg_g)
+                back = (gG.reshape(N * B, -1), rows, zG)
+        return (xv, zV, g_out), back
+
+    def critic_grads_v(self, vstate):
+        """Gradients of V's variables from critic_head's (rows, saves, dL/dV)."""
+        xv, zV, g_out = vstate
+        Vnet = self.model_critic.NN_value
+        with torch.no_grad():
             _, gV = ops.row_mlp_backward(Vnet.bn_rs, Vnet.trainable_variables(), xv, zV, g_out,
                                          False, True)
-            if fused:
-                g_gdot = ops.td_assemble_bwd_gdot(eqp, dt, coef, -g)
-                return gV, g_gdot.reshape(N * B), rows, zG, u_rows, dw_rows
-            gG = ops.td_assemble_bwd(eqp, x, u, d.dw, dt, coef, -g)
-        return gV, gG.reshape(N * B, -1), rows, zG
+        return gV
 
     def critic_G_back(self, front):
         """G's parameter gradients from critic_front's outputs (dpac_mlp_rows_bwd[_td1] +
@@ -711,20 +740,23 @@ class ActorCriticSolver(object):
             if cg is None:
                 if self._side_g is None:
                     self._side_g = torch.cuda.Stream()
-                cg = self._graphs[ckey] = _SplitCriticGraphs(self.critic_front, self.critic_G_back,
-                                                             dc, self._side_g)
+                cg = self._graphs[ckey] = _SplitCriticGraphs(self.critic_head, self.critic_grads_v,
+                                                             self.critic_G_back, dc, self._side_g)
             ccnt = dc.x0.shape[0]
             ctot = total or ccnt * self.par.world
-            gV = cg.front(dc)
-            front_done = torch.cuda.Event()
-            front_done.record()
-            gV = self.par.allreduce_grads(gV, ccnt, ctot)
+            cg.head(dc)
+            head_done = torch.cuda.Event()
+            head_done.record()
+            if GBACK == "early":  # G's backward beside V's update and the actor's terminal V
+                gG = cg.launch_back(head_done)
+            gV = self.par.allreduce_grads(cg.grads_v(), ccnt, ctot)
             # one Adam step of the critic in two parts: V now (the actor reads it), G beside the BPTT
             self.optimizer_critic.apply_gradients(
                 zip(gV, self.model_critic.NN_value.trainable_variables()), advance=False)
-        g = sg.grads()  # the BPTT is queued before G's backward, so it claims its CUs first
+        g = sg.grads()  # the actor's terminal V(x_N), BPTT and parameter gradients
         if cg is not None:
-            gG = cg.launch_back(front_done)
+            if GBACK != "early":
+                gG = cg.launch_back(head_done)
             with torch.cuda.stream(cg.side):
                 gG = self.par.allreduce_grads(gG, ccnt, ctot)
                 self.optimizer_critic.apply_gradients(

@@ -55,7 +55,7 @@ extern "C" {
  * (below) and the float fused rollout / BPTT (dpac_rollout_nn_fwd[_masked],
  * dpac_rollout_nn_bwd_masked) read them too.  Bindings must refuse a library of another
  * version. */
-#define DPAC_ABI_VERSION 4
+#define DPAC_ABI_VERSION 5
 
 /* status codes besides hipError_t values */
 #define DPAC_OK 0
@@ -441,6 +441,16 @@ int dpac_mlp_prepare(int32_t dtype, const dpac_mlp* net, double gamma_scale, voi
 int dpac_adam_apply(int32_t dtype, int32_t n_tensors, const int64_t* numel, void* const* var,
                     const void* const* grad, void* const* m, void* const* v, double alpha,
                     double beta_1, double beta_2, double epsilon, void* stream);
+
+/* ---- the critic loss's gradient at V's outputs (one launch) -------------
+ * loss_critic (solver.py:73-78) differentiated at V = NN_value([x_0; x_N; x_bdry]) (3B):
+ * delta = V0 − y − VN·disc, delta_b = Vb − z_bdry (solver.py:189-190), h'(z) = 2z for
+ * |z| < delta_clip else 2·delta_clip·sign(z); g = h'(delta)·scale, g_b = h'(delta_b)·scale;
+ * writes g_out = [g; −g·disc; g_b] (3B) and neg_g = −g (B, dL/dy for the TD backward).
+ * Rounds as the same tensor expressions do. */
+int dpac_critic_loss_grad(int32_t dtype, int64_t num_sample, const void* V, const void* y,
+                          const void* disc, const void* z_bdry, double scale, double delta_clip,
+                          void* g_out, void* neg_g, void* stream);
 
 /* ---- device equation coefficients (for parity tests and metrics) -------
  * Evaluates one Equation method row-wise on x [B][d] (and u [B][c] where the

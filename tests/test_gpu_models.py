@@ -5,6 +5,8 @@ The product (libdpac kernels + PyTorch MLPs on the GPU) and the oracle
 the same host-sampled inputs; losses and gradients must agree to 1e-9 relative
 (float64; the bound covers re-association inside GEMMs / reductions).
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -198,3 +200,34 @@ def test_sample_iteration_prefetch_keeps_the_sample_stream():
         for ga, rb in zip(got, ref):
             for x, y in zip(ga, rb):
                 assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_critic_loss_grad_kernel_matches_tensor_ops(dtype):
+    """dpac_critic_loss_grad (the critic loss's gradient at V's outputs, solver.py:73-78,
+    189-190) is bitwise the tensor expressions it replaces, including deltas past the Huber
+    clip on both sides and a zero delta; and rejects malformed calls."""
+    from deeppde_actorcritic_amd import _lib, ops
+    B = 1000
+    g = torch.Generator().manual_seed(3)
+    V = (torch.randn(3 * B, 1, generator=g, dtype=torch.float64) * 40).to(dtype).cuda()
+    y = (torch.randn(B, generator=g, dtype=torch.float64) * 40).to(dtype).cuda()
+    disc = torch.rand(B, generator=g, dtype=torch.float64).to(dtype).cuda()
+    zb = (torch.randn(B, 1, generator=g, dtype=torch.float64) * 40).to(dtype).cuda()
+    V[0, 0], y[0], V[B, 0] = 1.0, 1.0, 0.0  # delta = 0 exactly
+    g_out, neg_g = ops.critic_loss_grad(V, y, disc, zb, 100.0 / B, psol.DELTA_CLIP)
+    Vv = V[:, 0]
+    delta = Vv[:B] - y - Vv[B:2 * B] * disc
+    delta_b = Vv[2 * B:] - zb[:, 0]
+    gr = psol._huber_grad(delta) * (100.0 / B)
+    ref = torch.cat([gr, -gr * disc, psol._huber_grad(delta_b) * (100.0 / B)]).unsqueeze(1)
+    assert int((delta.abs() >= psol.DELTA_CLIP).sum()) > 10 and int((delta.abs() < psol.DELTA_CLIP).sum()) > 10
+    assert torch.equal(g_out, ref) and torch.equal(neg_g, -gr)
+    lib = _lib.load()
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    assert lib.dpac_critic_loss_grad(_lib.F32, 0, P(V), P(y), P(disc), P(zb), 1.0, 50.0, P(V), P(y),
+                                     None) == _lib.DPAC_EINVAL
+    assert lib.dpac_critic_loss_grad(_lib.F32, B, None, P(y), P(disc), P(zb), 1.0, 50.0, P(V), P(y),
+                                     None) == _lib.DPAC_EINVAL
+    assert lib.dpac_critic_loss_grad(_lib.F32, B, P(V), P(y), P(disc), P(zb), 1.0, 0.0, P(V), P(y),
+                                     None) == _lib.DPAC_EINVAL
