@@ -244,25 +244,35 @@ def cpu_baseline(seconds=8.0):
             "value": 2 * Bt * 100 / el, "unit": "traj-steps/s", "ms_per_iteration": el * 1e3,
             "sample": f"1 oracle training iteration (critic + actor step) on lqr_d20, {tag}, B={Bt}, "
                       f"N=100, 3x200 MLPs ({el:.1f} s)"}
-    # the same rollout on ALL of the host's cores (f64), a bounded sample
-    precision.set_dtype(torch.float64)
-    torch.set_num_threads(nproc)
-    eq = oeq.LQR(lqr_config())
-    np.random.seed(1234)
-    x0, dw, _ = eq.sample_normal(B_PER_GPU, HORIZON)
-    x0t, dwt = torch.as_tensor(x0), torch.as_tensor(dw)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        eq.propagate_adaptive(B_PER_GPU, x0t, dwt, None, False, T_TOTAL, HORIZON, True)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or reps >= 50:
-            break
-    progress(f"cpu_baseline rollout f64 on {nproc} threads: {reps} reps in {el:.1f} s")
-    entries["rollout_f64_all_cores"] = {
-        "value": reps * B_PER_GPU * HORIZON / el, "unit": "traj-steps/s", "cores": nproc,
-        "sample": f"{reps} x oracle propagate_adaptive(cheat=True), f64, B={B_PER_GPU}, d={DIM}, N={HORIZON}, "
-                  f"torch threads = nproc = {nproc} ({el:.1f} s)"}
+    # the same rollout on ALL of the host's cores (f64), a bounded sample — only where the job
+    # may use them: a GPU box allots each job a CPU share (OMP_NUM_THREADS, 16 per GPU) of a
+    # much larger host, and oversubscribing it stalls a single repetition for minutes
+    allotted = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if allotted and allotted < nproc:
+        entries["rollout_f64_all_cores"] = {
+            "value": None, "cores_visible": nproc, "cores_allotted": allotted,
+            "note": f"not run: this job is allotted {allotted} of the host's {nproc} CPUs "
+                    f"(OMP_NUM_THREADS); rollout_f64 above uses that share"}
+        progress(f"cpu_baseline all-cores entry skipped: {allotted} of {nproc} CPUs allotted")
+    else:
+        precision.set_dtype(torch.float64)
+        torch.set_num_threads(nproc)
+        eq = oeq.LQR(lqr_config())
+        np.random.seed(1234)
+        x0, dw, _ = eq.sample_normal(B_PER_GPU, HORIZON)
+        x0t, dwt = torch.as_tensor(x0), torch.as_tensor(dw)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            eq.propagate_adaptive(B_PER_GPU, x0t, dwt, None, False, T_TOTAL, HORIZON, True)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or reps >= 50:
+                break
+        progress(f"cpu_baseline rollout f64 on {nproc} threads: {reps} reps in {el:.1f} s")
+        entries["rollout_f64_all_cores"] = {
+            "value": reps * B_PER_GPU * HORIZON / el, "unit": "traj-steps/s", "cores": nproc,
+            "sample": f"{reps} x oracle propagate_adaptive(cheat=True), f64, B={B_PER_GPU}, d={DIM}, N={HORIZON}, "
+                      f"torch threads = nproc = {nproc} ({el:.1f} s)"}
     torch.set_num_threads(threads)
     head = entries["rollout_f64"]
     return {"value": head["value"], "unit": "traj-steps/s", "cores": threads, "kind": "port",

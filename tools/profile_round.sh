@@ -10,8 +10,10 @@ export TMPDIR=/tmp
 R=$PWD
 rm -f gpurun_out/steps.log
 rm -rf gpurun_out/prof_kt gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof_train
-run 900 pytest_gpu python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread
-run 300 smoke python -u -c "import __graft_entry__ as g; g.smoke()"
+if [ -z "${SKIP_TESTS:-}" ]; then
+  run 900 pytest_gpu python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread
+  run 300 smoke python -u -c "import __graft_entry__ as g; g.smoke()"
+fi
 run 400 bench python -u bench.py --steps 200 --warmup 20
 run 300 prof_kt rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-train
 run 60 headline python tools/rocprof_headline.py gpurun_out/prof_kt/run_kernel_trace.csv gpurun_out/prof_kt.log --steps 100 --warmup 10
