@@ -51,14 +51,18 @@ PgArgs<T> pg_args(const dpac_mlp& net, int64_t rows, const void* x, int64_t ldx,
 #ifndef DPAC_PG_CHUNKS
 #define DPAC_PG_CHUNKS 256  // 2 workgroups per CU on the wide layers (measured 819 -> 681 us at 204800 rows)
 #endif
+#ifndef DPAC_PG_MIN_ROWS
+#define DPAC_PG_MIN_ROWS 256  // rows per chunk at least: small row counts (the critic's V over 3B rows)
+#endif                        // would otherwise write and re-read ~256 near-empty partials
 template <typename T>
 int64_t pg_chunk_rows(int64_t rows, int64_t max_ld) {
-  // DPAC_PG_CHUNKS chunks: the wide layers' two column groups give 2 workgroups
-  // per CU, the narrow ones one, and a partial buffer the reduce reads in
-  // ~25 us.  A chunk's rows are addressed
-  // through 32-bit buffer descriptors: keep them below 2 GiB.
+  // DPAC_PG_CHUNKS chunks of at least DPAC_PG_MIN_ROWS rows: the wide layers' two column
+  // groups give 2 workgroups per CU, the narrow ones one, and a partial buffer the reduce
+  // reads in ~25 us.  A chunk's rows are addressed through 32-bit buffer descriptors: keep
+  // them below 2 GiB.
   constexpr int SR = PgCfg<T>::SR;
   int64_t per = (rows + DPAC_PG_CHUNKS - 1) / DPAC_PG_CHUNKS;
+  per = std::max<int64_t>(per, DPAC_PG_MIN_ROWS);
   const int64_t cap = (((int64_t)1 << 31) - 1) / (max_ld * (int64_t)sizeof(T)) / SR * SR;
   per = (per + SR - 1) / SR * SR;
   return std::max<int64_t>(std::min(per, cap), SR);
