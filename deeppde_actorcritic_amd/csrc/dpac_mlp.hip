@@ -156,7 +156,8 @@ inline bool pg_x3(const dpac_mlp& net) {
 }
 
 // one layer of the split-fp16 kernel: wide outputs 1 x 8 waves (one column tile each,
-// 128-column groups), outputs of <= 32 columns 8 x 1 waves over the row tiles
+// 128-column groups: two column tiles per wave, one 256-column group, measured 292 bytes of
+// spills at 13 input tiles), outputs of <= 32 columns 8 x 1 waves over the row tiles
 int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   const int K = a.width[l], H = a.width[l + 1];
   const int nti = (K + 15) / 16;

@@ -21,15 +21,16 @@
 // Workgroup (chunk c, column group g, layer l) = 8 wavefronts; a sub-chunk of 32 rows is
 // staged through LDS per step:
 //  * staging: thread (rb = tid / 128, f = tid % 128) loads rows 8 rb .. 8 rb + 7 of A feature
-//    f (+128) and of B column f — coalesced dword loads along the row — applies BN and the
+//    f (+128) and of B column f (+128) — coalesced dword loads along the row — applies BN and the
 //    activation (A) or the BN scale (B), splits, and writes each 8-row run as ONE 16-byte LDS
 //    write per part: the images are [part][row block][feature][8 rows] halves, which is
 //    exactly the MFMA fragment order (lane l reads feature l & 15, row block l >> 4), so a
 //    fragment read is 4 runs of 256 contiguous bytes;
 //  * MFMA: wave (wi, wj) of a WI x WJ grid owns row tiles wi + WI ti (features of layer l)
 //    and column tiles wj + WJ jj of the group.  Wide layers: WI = 1, WJ = 8, one column tile
-//    per wave (CW = 128 columns, 2 groups at H = 200); outputs of <= 32 columns: WI = 8,
-//    WJ = 1 (the waves split the row tiles).
+//    per wave (CW = 128 columns, 2 groups at H = 200; NTJ = 2 would stage A once per chunk
+//    but needs > 256 VGPRs at 13 input tiles); outputs of <= 32 columns: WI = 8, WJ = 1 (the
+//    waves split the row tiles).
 // Partials go to the same [chunk][ptot] layout k_param_grads_reduce sums.
 #pragma once
 
@@ -51,12 +52,12 @@ static_assert(kPgxDepth == 1 || kPgxDepth == 2, "1 or 2 stages");
 constexpr float kPgxLo = 4096.f, kPgxLoInv = 1.f / 4096.f;
 
 // staged values of one sub-chunk (registers; loaded before the previous sub-chunk's MFMAs)
-template <int QA, bool L0>
+template <int QA, int QB, bool L0>
 struct PgxStage {
   float a[QA][8];             // zin_l at rows 8 rb + i, features f + 128 q
   float g0[L0 ? QA : 1][8];   // layer 0: G_0 at the same places (BN_0 sums)
-  float gb[8];      // G_{l+1} at column col0 + f
-  float zb[8];      // zin_{l+1} (pre-bias) at the same places
+  float gb[QB][8];            // G_{l+1} at columns col0 + f + 128 q
+  float zb[QB][8];            // zin_{l+1} (pre-bias) at the same places
 };
 
 __device__ __forceinline__ void pgx_split8(const float (&v)[8], pgh8& h, pgh8& l) {
@@ -70,16 +71,17 @@ __device__ __forceinline__ void pgx_split8(const float (&v)[8], pgh8& h, pgh8& l
 template <int NTI, int NTJ, int WI, bool L0>
 __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<float> a, const int l) {
   constexpr int WJ = kPgxWaves / WI;
-  constexpr int CW = 16 * NTJ * WJ;                     // B columns per workgroup (<= 128)
+  constexpr int CW = 16 * NTJ * WJ;                     // B columns per workgroup (<= 256)
   constexpr int KP = 16 * NTI * WI;                     // staged A features
   constexpr int QA = (KP + 127) / 128;                  // A features per staging thread
-  static_assert(CW <= 128 && KP <= DPAC_MLP_MAX_WIDTH, "staging map: 128 columns, 256 features");
+  constexpr int QB = (CW + 127) / 128;                  // B columns per staging thread
+  static_assert(CW <= 256 && KP <= DPAC_MLP_MAX_WIDTH, "staging map: 256 columns, 256 features");
   // LDS: the images, halves A [2 parts][4 row blocks][KP][8], B [3][4][CW][8] (hi, lo,
   // 2^12 hi); after the
-  // row loop the same bytes hold the BN column sums' reduction ([4 rb][2][128] floats for
+  // row loop the same bytes hold the BN column sums' reduction ([4 rb][2][CW] floats for
   // the B side, then [4 rb][2][128 QA] for BN_0 on the input layer)
   constexpr int kImgBytes = (2 * KP + 3 * CW) * 4 * 8 * 2;
-  constexpr int kRedFloats = 4 * 2 * 128 + (L0 ? 4 * 2 * 128 * QA : 0);
+  constexpr int kRedFloats = 4 * 2 * CW + (L0 ? 4 * 2 * 128 * QA : 0);
   constexpr int kMain = kImgBytes > kRedFloats * 4 ? kImgBytes : kRedFloats * 4;
   // then the column scaling: sub-chunk maxima [4 rb][CW], rescale factors [CW], exponents [CW]
   constexpr int kSmem = kMain + (4 * CW + 2 * CW) * 4;
@@ -120,13 +122,20 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
     offA[q] = v ? (uint32_t)k * 4u : kOOB;
     offG0[q] = (v && first) ? (uint32_t)k * 4u : kOOB;
   }
-  const int hcol = col0 + fl;
-  const bool bv = fl < CW && hcol < H;
-  const float sbv = bv ? a.scale[l + 1][hcol] : 0.f;
-  const float bbv = (bv && last) ? a.bias[hcol] : 0.f;
-  const uint32_t offB = bv ? (uint32_t)fl * 4u : kOOB;
-  float cs0_b[QA], cs0_s[QA], csb_b = 0.f, csb_s = 0.f;
-  int cexp = -100;  // the column's running exponent (B staging threads)
+  float sbv[QB], bbv[QB], csb_b[QB], csb_s[QB];
+  uint32_t offB[QB];
+  int cexp[QB];  // the columns' running exponents (B staging threads)
+#pragma unroll
+  for (int q = 0; q < QB; ++q) {
+    const int c = fl + 128 * q, hcol = col0 + c;
+    const bool bv = c < CW && hcol < H;
+    sbv[q] = bv ? a.scale[l + 1][hcol] : 0.f;
+    bbv[q] = (bv && last) ? a.bias[hcol] : 0.f;
+    offB[q] = bv ? (uint32_t)c * 4u : kOOB;
+    csb_b[q] = csb_s[q] = 0.f;
+    cexp[q] = -100;
+  }
+  float cs0_b[QA], cs0_s[QA];
 #pragma unroll
   for (int q = 0; q < QA; ++q) cs0_b[q] = cs0_s[q] = 0.f;
   pgf4 acc[NTI][NTJ];  // 2^12 x (the column-scaled) dW tile
@@ -137,7 +146,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
 
   // loads of the 32 rows at r0: descriptors based at row r0 ending at the chunk's last row
   // (rows past it read 0, so their G is 0 and they add nothing); masked columns carry kOOB
-  auto issue = [&](int64_t r0, PgxStage<QA, L0>& st) {
+  auto issue = [&](int64_t r0, PgxStage<QA, QB, L0>& st) {
     const int64_t nr = r_end - r0;  // >= 1
     const auto rA = make_rsrc(srcA + r0 * ldA, (uint32_t)(((nr - 1) * ldA + K) * 4));
     const auto rG = make_rsrc(gA + r0 * a.gtot, (uint32_t)(((nr - 1) * a.gtot + K) * 4));
@@ -151,15 +160,18 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
         st.a[q][i] = buf_load_elem<float>(rA, offA[q] + r * (uint32_t)ldA * 4u);
         if constexpr (L0) st.g0[q][i] = first ? buf_load_elem<float>(rG, offG0[q] + r * (uint32_t)a.gtot * 4u) : 0.f;
       }
-      st.gb[i] = buf_load_elem<float>(rB, offB + r * (uint32_t)a.gtot * 4u);
-      st.zb[i] = buf_load_elem<float>(rZ, offB + r * (uint32_t)a.ztot * 4u);
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        st.gb[q][i] = buf_load_elem<float>(rB, offB[q] + r * (uint32_t)a.gtot * 4u);
+        st.zb[q][i] = buf_load_elem<float>(rZ, offB[q] + r * (uint32_t)a.ztot * 4u);
+      }
     }
   };
 
   const int fq = lane >> 4, fi = lane & 15;  // fragment: row block, feature / column in the tile
   // one sub-chunk of 32 rows from its staged registers `st`, which are then refilled with
   // the sub-chunk kPgxDepth ahead (kPgxDepth register stages in flight)
-  auto sub = [&](int64_t r0, PgxStage<QA, L0>& st) {
+  auto sub = [&](int64_t r0, PgxStage<QA, QB, L0>& st) {
     __syncthreads();  // the previous sub-chunk's fragment reads are done
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
@@ -181,43 +193,49 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
       *reinterpret_cast<pgh8*>(sA + ((0 * 4 + rb) * KP + k) * 8) = h;
       *reinterpret_cast<pgh8*>(sA + ((1 * 4 + rb) * KP + k) * 8) = lo;
     }
-    float vb[8];
-    if (fl < CW) {
+    float vb[QB][8];
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int c = fl + 128 * q;
+      if (c >= CW) continue;  // compile-time for q = 0 when CW >= 128
       float m = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float gv = st.gb[i];
-        vb[i] = gv * sbv;
-        m = fmaxf(m, fabsf(vb[i]));
-        csb_b += gv;
-        csb_s += gv * (st.zb[i] + bbv);  // bbv = 0 unless the output layer
+        const float gv = st.gb[q][i];
+        vb[q][i] = gv * sbv[q];
+        m = fmaxf(m, fabsf(vb[q][i]));
+        csb_b[q] += gv;
+        csb_s[q] += gv * (st.zb[q][i] + bbv[q]);  // bbv = 0 unless the output layer
       }
-      s_cmax[rb * CW + fl] = m;
+      s_cmax[rb * CW + c] = m;
     }
     __syncthreads();  // the column maxima of the sub-chunk
-    if (fl < CW) {
-      const float m = fmaxf(fmaxf(s_cmax[fl], s_cmax[CW + fl]), fmaxf(s_cmax[2 * CW + fl], s_cmax[3 * CW + fl]));
-      int e = cexp;
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int c = fl + 128 * q;
+      if (c >= CW) continue;
+      const float m = fmaxf(fmaxf(s_cmax[c], s_cmax[CW + c]), fmaxf(s_cmax[2 * CW + c], s_cmax[3 * CW + c]));
+      int e = cexp[q];
       if (m > 0.f && m < 3.0e38f) {
         int em = 0;
         (void)frexpf(m, &em);  // m in [2^(em-1), 2^em)
-        e = em > cexp ? em : cexp;
+        e = em > cexp[q] ? em : cexp[q];
       }
       const float sc = ldexpf(1.f, 3 - e);  // the column's values times sc: |v| < 8
 #pragma unroll
-      for (int i = 0; i < 8; ++i) vb[i] *= sc;
+      for (int i = 0; i < 8; ++i) vb[q][i] *= sc;
       pgh8 h, lo, h12;
-      pgx_split8(vb, h, lo);
+      pgx_split8(vb[q], h, lo);
 #pragma unroll
       for (int i = 0; i < 8; ++i) h12[i] = h[i] * (_Float16)kPgxLo;  // exact: |h| < 8
-      *reinterpret_cast<pgh8*>(sB + ((0 * 4 + rb) * CW + fl) * 8) = h;
-      *reinterpret_cast<pgh8*>(sB + ((1 * 4 + rb) * CW + fl) * 8) = lo;
-      *reinterpret_cast<pgh8*>(sB + ((2 * 4 + rb) * CW + fl) * 8) = h12;
+      *reinterpret_cast<pgh8*>(sB + ((0 * 4 + rb) * CW + c) * 8) = h;
+      *reinterpret_cast<pgh8*>(sB + ((1 * 4 + rb) * CW + c) * 8) = lo;
+      *reinterpret_cast<pgh8*>(sB + ((2 * 4 + rb) * CW + c) * 8) = h12;
       if (rb == 0) {
-        s_cfac[fl] = ldexpf(1.f, cexp - e);  // the accumulated column, to the new scale (exact)
-        s_cexp[fl] = e;
+        s_cfac[c] = ldexpf(1.f, cexp[q] - e);  // the accumulated column, to the new scale (exact)
+        s_cexp[c] = e;
       }
-      cexp = e;
+      cexp[q] = e;
     }
     __syncthreads();
     if (r0 + kPgxDepth * kPgxSR < r_end) issue(r0 + kPgxDepth * kPgxSR, st);  // lands kPgxDepth sub-chunks later
@@ -257,12 +275,12 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
       xl = nl;
     }
   };
-  PgxStage<QA, L0> st0;
+  PgxStage<QA, QB, L0> st0;
   issue(r_begin, st0);
   if constexpr (kPgxDepth == 1) {
     for (int64_t r0 = r_begin; r0 < r_end; r0 += kPgxSR) sub(r0, st0);
   } else {
-    PgxStage<QA, L0> st1;
+    PgxStage<QA, QB, L0> st1;
     if (r_begin + kPgxSR < r_end) issue(r_begin + kPgxSR, st1);
     for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * kPgxSR) {
       sub(r0, st0);
@@ -290,9 +308,15 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
   // ---- BN column sums: combine the 4 row blocks through LDS (reusing the images) ----
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
-  float* red0 = red + 4 * 2 * 128;
-  red[(rb * 2 + 0) * 128 + fl] = csb_b;
-  red[(rb * 2 + 1) * 128 + fl] = csb_s;
+  float* red0 = red + 4 * 2 * CW;
+#pragma unroll
+  for (int q = 0; q < QB; ++q) {
+    const int c = fl + 128 * q;
+    if (c < CW) {
+      red[(rb * 2 + 0) * CW + c] = csb_b[q];
+      red[(rb * 2 + 1) * CW + c] = csb_s[q];
+    }
+  }
   if constexpr (L0) {
     if (first) {
 #pragma unroll
@@ -307,8 +331,8 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
     float sb = 0.f, ss = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      sb += red[(w * 2 + 0) * 128 + tid];
-      ss += red[(w * 2 + 1) * 128 + tid];
+      sb += red[(w * 2 + 0) * CW + tid];
+      ss += red[(w * 2 + 1) * CW + tid];
     }
     part[a.off_beta[l + 1] + col0 + tid] = sb;
     part[a.off_gamma[l + 1] + col0 + tid] = ss;

