@@ -15,6 +15,9 @@ rows [off, off+cnt) of that batch) and compares every parameter; then train() en
 the single-process train().  Cases: lqr_var_d20 (BASELINE configs[3]) and vdp_d20
 (configs[4]) at d = 20 with TD1, lqr_var_d20 with TD2 (no G network: no split critic).
 Writes one JSON object (max relative differences) and exits non-zero past 1e-12.
+With --backend nccl every collective of that path runs on RCCL (the seed broadcast on a
+device tensor, the gradient all-reduces on the current and the side stream, the metric
+reductions, the device all-gather of the final arrays); a one-GPU box runs it as one rank.
 """
 import argparse
 import json
@@ -73,14 +76,17 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--batch", type=int, default=40)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
+                    help="nccl (= RCCL): one rank per GPU, so on a one-GPU box a single rank")
     a = ap.parse_args()
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    dist.init_process_group(a.backend)
     from deeppde_actorcritic_amd.config import set_floatx
     from deeppde_actorcritic_amd.parallel import DataParallel
     set_floatx("float64")
     rank, world = dist.get_rank(), dist.get_world_size()
-    res = {"world": world, "backend": "gloo (ranks share cuda:0)", "tol": TOL, "cases": []}
+    res = {"world": world, "backend": "gloo (ranks share cuda:0)" if a.backend == "gloo" else
+           f"nccl = RCCL, {world} rank(s), one GPU each", "tol": TOL, "cases": []}
     ok = True
     B, N = a.batch, 10
     for name, td in CASES:
@@ -110,7 +116,7 @@ def main():
         os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)
-    flag = torch.tensor([0 if ok else 1])
+    flag = torch.tensor([0 if ok else 1], device="cuda" if a.backend == "nccl" else "cpu")
     dist.broadcast(flag, 0)
     dist.destroy_process_group()
     sys.exit(int(flag.item()))

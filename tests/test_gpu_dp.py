@@ -39,3 +39,23 @@ def test_two_rank_training_equals_single_process(tmp_path):
     for c in res["cases"]:
         assert c["params_max_rel_diff"] <= 1e-12 and c["history_max_rel_diff"] <= 1e-12
         assert c["final_arrays_rows"] == c["batch"]
+
+
+def test_rccl_single_rank_path_equals_single_process(tmp_path):
+    """The same script on RCCL ("nccl" backend) with one rank on cuda:0: every collective the
+    data-parallel product path issues (broadcast of the seed on a device tensor, the gradient
+    all-reduces on the current and the side stream inside the training step, the metric
+    reductions, the device all-gather of the final arrays) executes on RCCL, and the results
+    equal the process-group-free path."""
+    out = tmp_path / "dp_nccl.json"
+    env = dict(os.environ, OMP_NUM_THREADS="4", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dp_equality.py"), "--backend", "nccl", "--out", str(out)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["ok"] and res["world"] == 1 and res["backend"].startswith("nccl")
+    for c in res["cases"]:
+        assert c["params_max_rel_diff"] <= 1e-12 and c["history_max_rel_diff"] <= 1e-12
+        assert c["final_arrays_rows"] == c["batch"]
