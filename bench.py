@@ -36,6 +36,7 @@ B_PER_GPU, DIM, HORIZON, T_TOTAL = 4096, 20, 200, 0.2
 N_SETS = 5  # rotating buffer sets: 5 x 138 MB (f32) > the 256 MiB Infinity Cache
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
+MFMA_F16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA dense peak (~2.5 PF)
 MLP_FLOP_PER_ROW = 2 * (20 * 200 + 200 * 200 * 2 + 200 * 20)  # 176 000
 
 
@@ -417,11 +418,18 @@ def main():
         w4, pl4 = time_launches(nn_launch, k4, 2, world)
         flops = MLP_FLOP_PER_ROW * B * N
         tfs = flops / (pl4 * 1e-3) / 1e12
+        x3 = dtype == torch.float32 and ops.MLP_MATH == "x3"
         variants["rollout_nn_fused"] = {
             "traj_steps_per_s": world * B * N * k4 / max_over_ranks(w4, world), "avg_launch_ms": pl4,
-            "mlp": "20-200-200-200-20",
+            "mlp": "20-200-200-200-20", "mlp_math": ops_mlp_math(dtype),
             "roofline": {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": tfs / MFMA_F32_PEAK_TFS, "kernel": "dpac::k_rollout_nn"}}
+                         "frac": tfs / MFMA_F32_PEAK_TFS,
+                         "kernel": "dpac::k_rollout_nn_x3" if x3 else "dpac::k_rollout_nn",
+                         "note": "achieved in f32-equivalent flops (176 kFLOP per trajectory-step) against the "
+                                 "f32-input MFMA peak"
+                                 + ("; the split-fp16 products' own ceiling is the fp16 dense peak / 3 = "
+                                    f"{MFMA_F16_PEAK_TFS / 3:.0f} TFLOP/s f32-equivalent: "
+                                    f"frac {tfs / (MFMA_F16_PEAK_TFS / 3):.3f} of that" if x3 else "")}}
         del rs, nn_out
         torch.cuda.empty_cache()
         if not args.no_train:
