@@ -47,7 +47,10 @@ constexpr int kX3Threads = 64 * kX3Waves;
 constexpr int kX3RT = 4;                  // row tiles per workgroup
 constexpr int kX3Rows = 16 * kX3RT;       // 64 rows
 constexpr int kX3MaxChunks = (DPAC_MLP_MAX_WIDTH + 31) / 32;  // 8
-constexpr int kX3Ld = 64 * kX3MaxChunks + 16;                 // halves per LDS row (1056 B)
+#ifndef DPAC_X3_LDPAD
+#define DPAC_X3_LDPAD 16  // halves of padding per LDS row (a multiple of 8: 16-byte rows)
+#endif
+constexpr int kX3Ld = 64 * kX3MaxChunks + DPAC_X3_LDPAD;      // halves per LDS row (1056 B at 16)
 constexpr float kX3LoScale = 4096.f;      // 2^12
 constexpr float kX3LoInv = 1.f / 4096.f;
 constexpr int kX3MaxNT = (DPAC_MLP_MAX_WIDTH / 16 + kX3Waves - 1) / kX3Waves;  // 2

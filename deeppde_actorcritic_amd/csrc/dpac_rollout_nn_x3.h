@@ -44,7 +44,10 @@ typedef _Float16 nxh8 __attribute__((ext_vector_type(8)));
 typedef _Float16 nxh4 __attribute__((ext_vector_type(4)));
 typedef float nxf4 __attribute__((ext_vector_type(4)));
 
-constexpr int kNxLd = 64 * 8 + 16;   // halves per row of a hidden image (K <= 256): 264 dwords = 8 mod 64
+#ifndef DPAC_NX_LDPAD
+#define DPAC_NX_LDPAD 16  // halves of padding per image row (a multiple of 8: 16-byte rows)
+#endif
+constexpr int kNxLd = 64 * 8 + DPAC_NX_LDPAD;  // halves per row of a hidden image (K <= 256): 264 dwords = 8 mod 64
 constexpr int kNxLd0 = 64 + 8;       // halves per row of the narrow input image (K <= 32): 36 dwords
 constexpr int kNxPartLd = 36;        // floats per row of a split-K partial (conflict-free b128 writes)
 constexpr int kNxWide = 7;           // 32-k chunks of a 193..224-wide K
