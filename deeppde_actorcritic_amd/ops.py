@@ -546,13 +546,18 @@ class _RowMLP(torch.autograd.Function):
         return (g_x, None, *(grads if grads is not None else [None] * len(params)))
 
 
-def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, ws_tag: int = 0):
+def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, ws_tag: int = 0,
+                     prepared=None):
     """The backward of mlp_rows(save=True) given dL/d(output) g_out [R, w_out]:
     dpac_mlp_rows_bwd (the input-gradient chain: G of every BN output, and dL/dx if
     want_x) then dpac_mlp_param_grads (if want_params).  params =
-    DeepNN.trainable_variables(); returns (g_x or None, parameter gradients or None)."""
-    L, gam, bet, Ws, b = _split_params(params)
-    view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, False, True)
+    DeepNN.trainable_variables(); prepared = mlp_prepare(..., want_wt=True) of the same
+    parameters if the caller already has it (one launch fewer); returns (g_x or None,
+    parameter gradients or None)."""
+    if prepared is None:
+        L, gam, bet, Ws, b = _split_params(params)
+        prepared = mlp_prepare(gam, bet, Ws, b, False, True)
+    view, wt, wt_km = prepared
     R = x.shape[0]
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
     g_x = torch.empty(R, view.widths[0], dtype=x.dtype, device=x.device) if want_x else None

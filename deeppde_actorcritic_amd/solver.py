@@ -120,6 +120,12 @@ class DeepNN(nn.Module):
         return 1 <= len(self.sizes) - 2 <= _lib.MLP_MAX_HIDDEN and max(self.sizes) <= _lib.MLP_MAX_WIDTH
 
     @torch.no_grad()
+    def mlp_prepared(self):
+        """(view, weight_t, weight_t_km) of mlp_prepare with the backward images too: one
+        launch for a forward over rows and its backward (ops.row_mlp_backward(prepared=))."""
+        return ops.mlp_prepare([g.detach() for g in self.bn_gamma], [bt.detach() for bt in self.bn_beta],
+                               [w.detach() for w in self.W], self.b.detach(), self.ekn_head, True)
+
     def mlp_view(self):
         """This network as dpac_rollout_nn_fwd reads it (BN scale = rs * gamma, the same
         product forward() forms)."""
@@ -298,6 +304,13 @@ class TFAdam:
         return {"iterations": self.iterations}
 
 
+# HIP-graph captures are thread-local: with a torch.distributed "nccl" (RCCL) process group
+# alive, its watchdog thread queries events concurrently, and under the default global
+# capture mode such a query invalidates an ongoing capture ("operation failed due to a
+# previous error during capture", seen intermittently in round 3's RCCL test).
+_CAPTURE_MODE = "thread_local"
+
+
 class _GradGraph:
     """One gradient evaluation (forward + backward, no optimizer step) captured as a
     HIP graph over static input buffers.  Replaying it after copying a fresh batch
@@ -316,7 +329,7 @@ class _GradGraph:
                 fn(self.static)
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode=_CAPTURE_MODE):
             self.out = fn(self.static)
 
     def __call__(self, batch: TrajectoryBatch):
@@ -343,9 +356,9 @@ class _SplitActorGraphs:
                 bwd_fn(fwd_fn(self.static))
         torch.cuda.current_stream().wait_stream(side)
         self.g_fwd, self.g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fwd):
+        with torch.cuda.graph(self.g_fwd, capture_error_mode=_CAPTURE_MODE):
             self.fwd = fwd_fn(self.static)
-        with torch.cuda.graph(self.g_bwd):
+        with torch.cuda.graph(self.g_bwd, capture_error_mode=_CAPTURE_MODE):
             self.out = bwd_fn(self.fwd)
 
     def launch_forward(self, batch: TrajectoryBatch):
@@ -383,11 +396,11 @@ class _SplitCriticGraphs:
                 back_fn((None,) + tuple(h[1]))
         torch.cuda.current_stream().wait_stream(side)
         self.g_head, self.g_v, self.g_back = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_head):
+        with torch.cuda.graph(self.g_head, capture_error_mode=_CAPTURE_MODE):
             self.head_out = head_fn(self.static)
-        with torch.cuda.graph(self.g_v):
+        with torch.cuda.graph(self.g_v, capture_error_mode=_CAPTURE_MODE):
             self.v_out = v_fn(self.head_out[0])
-        with torch.cuda.graph(self.g_back):
+        with torch.cuda.graph(self.g_back, capture_error_mode=_CAPTURE_MODE):
             self.back_out = back_fn((None,) + tuple(self.head_out[1]))
 
     def head(self, batch: TrajectoryBatch):
@@ -616,9 +629,10 @@ class ActorCriticSolver(object):
             Vnet = self.model_critic.NN_value
             with torch.no_grad():
                 xN = xN.contiguous()
-                v, zV = ops.mlp_rows(Vnet.mlp_view(), xN, save=True)
+                prep = Vnet.mlp_prepared()  # forward and backward images, one launch
+                v, zV = ops.mlp_rows(prep[0], xN, save=True)
                 gV, _ = ops.row_mlp_backward(Vnet.bn_rs, [p.detach() for p in Vnet.trainable_variables()],
-                                             xN, zV, torch.ones_like(v), True, False)
+                                             xN, zV, torch.ones_like(v), True, False, prepared=prep)
             term = v[:, 0]
         else:
             xl = xN.detach().requires_grad_(True)
@@ -654,7 +668,7 @@ class ActorCriticSolver(object):
         100*(mean h(delta) + mean h(delta_bdry)) (solver.py:73-78, 189-190) differentiated by
         hand at V's output and at G: h'(z) = 2z inside |z| < 50, 100 sign(z) outside;
         dL/dV(x_0) = g, dL/dV(x_N) = -g*disc, dL/dy = -g, dL/dV(x_bdry) = g_bdry.
-        Returns ((V's rows, V's saves, dL/dV), the G backward's inputs)."""
+        Returns ((V's rows, V's saves, dL/dV, V's prepared images), the G backward's inputs)."""
         mc, ec = self.model_critic, self.eqn_config
         d = Equation.to_native(data, self.dtype)
         N, T = ec.num_time_interval_critic, ec.total_time_critic
@@ -676,7 +690,8 @@ class ActorCriticSolver(object):
                 y, disc = ops.td_assemble(eqp, mc.td, x, u, d.dw, dt, coef, G.view(N, B, -1),
                                           cost_order=_lib.COST_CRITIC)
             xv = torch.cat([x[0], x[N], d.x_bdry])
-            Vout, zV = ops.mlp_rows(Vnet.mlp_view(), xv, save=True)
+            prepV = Vnet.mlp_prepared()  # V's forward and backward images, one launch
+            Vout, zV = ops.mlp_rows(prepV[0], xv, save=True)
             # delta = V(x_0) - y - V(x_N) disc, delta_b = V(x_bdry) - Z_tf(x_bdry)
             # (solver.py:189-190) and the Huber gradient, one launch
             g_out, neg_g = ops.critic_loss_grad(Vout, y, disc, self.bsde.Z_tf(d.x_bdry), 100.0 / B, DELTA_CLIP)
@@ -686,15 +701,16 @@ class ActorCriticSolver(object):
             else:
                 gG = ops.td_assemble_bwd(eqp, x, u, d.dw, dt, coef, neg_g)
                 back = (gG.reshape(N * B, -1), rows, zG)
-        return (xv, zV, g_out), back
+        return (xv, zV, g_out, prepV), back
 
     def critic_grads_v(self, vstate):
-        """Gradients of V's variables from critic_head's (rows, saves, dL/dV)."""
-        xv, zV, g_out = vstate
+        """Gradients of V's variables from critic_head's (rows, saves, dL/dV, V's prepared
+        images)."""
+        xv, zV, g_out, prepV = vstate
         Vnet = self.model_critic.NN_value
         with torch.no_grad():
             _, gV = ops.row_mlp_backward(Vnet.bn_rs, Vnet.trainable_variables(), xv, zV, g_out,
-                                         False, True)
+                                         False, True, prepared=prepV)
         return gV
 
     def critic_G_back(self, front):
