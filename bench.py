@@ -249,6 +249,10 @@ def cpu_baseline(seconds=8.0):
     # may use them: a GPU box allots each job a CPU share (OMP_NUM_THREADS, 16 per GPU) of a
     # much larger host, and oversubscribing it stalls a single repetition for minutes
     allotted = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    try:
+        allotted = min(allotted or nproc, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
     if allotted and allotted < nproc:
         entries["rollout_f64_all_cores"] = {
             "value": None, "cores_visible": nproc, "cores_allotted": allotted,
