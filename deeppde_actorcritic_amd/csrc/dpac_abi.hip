@@ -9,8 +9,8 @@
 
 namespace dpac {
 // The instantiation table the equation TUs fill at load time (Registrar, dpac_kernels.h):
-// [equation id][dim][f64].  Zero-initialised before any constructor runs.
-constexpr int kMaxRegDim = 64;
+// [equation id][dim][f64] (dim up to kMaxRegDim, dpac_kernels.h, checked at build time by
+// Registrar).  Zero-initialised before any constructor runs.
 static DispatchFn g_dispatch[4][kMaxRegDim + 1][2];
 void register_dispatch(int eqn, int dim, int f64, DispatchFn fn) {
   if (eqn >= 0 && eqn < 4 && dim >= 1 && dim <= kMaxRegDim && (f64 == 0 || f64 == 1)) g_dispatch[eqn][dim][f64] = fn;

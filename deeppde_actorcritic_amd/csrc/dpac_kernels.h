@@ -1420,9 +1420,12 @@ int run_op(const OpArgs& a) {
 using DispatchFn = int (*)(const OpArgs&);
 void register_dispatch(int eqn, int dim, int f64, DispatchFn fn);
 DispatchFn find_dispatch(int eqn, int dim, int f64);
+constexpr int kMaxRegDim = 64;  // the dispatch table's dimension range (dpac_abi.hip)
 
 template <template <typename, int> class EQ, typename T, int... Ds>
 struct Registrar {
+  static_assert(((Ds >= 1 && Ds <= kMaxRegDim) && ...),
+                "DPAC_DIMS holds a dimension outside the dispatch table (1..kMaxRegDim)");
   explicit Registrar(int eqn) {
     (register_dispatch(eqn, Ds, std::is_same<T, double>::value ? 1 : 0, &run_op<T, EQ<T, Ds>, Ds>), ...);
   }

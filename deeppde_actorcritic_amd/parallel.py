@@ -5,7 +5,10 @@ independent (equation.py:53-69) and every loss is a batch mean (solver.py:76-77,
 82), so rank r owns global trajectories [offset_r, offset_r + count_r) of every
 batch and the only exchange is one all-reduce of the flattened gradient per
 optimizer step (RCCL over xGMI with the "nccl" backend; gloo on CPU in tests),
-plus tiny SUM / MAX reductions for the validation metrics.
+plus tiny SUM / MAX reductions for the validation metrics.  A training iteration
+(solver.py:67-70) issues two gradient all-reduces: V's half of the critic step (the
+actor's terminal value V(x_N) needs the updated V, solver.py:221), then the actor's
+gradients and the critic's G half together (allreduce_grads_multi), SURVEY §8(e).
 """
 from __future__ import annotations
 
@@ -29,6 +32,7 @@ class DataParallel:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.grad_allreduces = 0  # gradient all-reduces issued (tests count them per iteration)
 
     def shard(self, total: int):
         return shard_range(total, self.rank, self.world)
@@ -40,21 +44,34 @@ class DataParallel:
         summed in ONE flattened all-reduce.  None entries (unused parameters, e.g. G
         under TD2) stay None; they are None on every rank.
         """
-        present = [g for g in grads if g is not None]
-        if not present:
-            return list(grads)
-        flat = torch.cat([g.reshape(-1) for g in present])
-        flat.mul_(count / total)
+        return self.allreduce_grads_multi([(grads, count, total)])[0]
+
+    def allreduce_grads_multi(self, parts):
+        """Several gradient lists, each (grads, count, total) with its own shard weight
+        count/total, summed over the ranks in ONE flattened all-reduce: [grads reduced] per
+        part, in order (e.g. the actor's gradients and the critic's G half, solver.py:88,95)."""
+        pieces = []
+        for grads, count, total in parts:
+            present = [g.reshape(-1) for g in grads if g is not None]
+            if present:
+                pieces.append(torch.cat(present).mul_(count / total))
+        if not pieces:
+            return [list(grads) for grads, _, _ in parts]
+        flat = torch.cat(pieces) if len(pieces) > 1 else pieces[0]
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-        out, i = [], 0
-        for g in grads:
-            if g is None:
-                out.append(None)
-                continue
-            n = g.numel()
-            out.append(flat[i:i + n].view_as(g))
-            i += n
-        return out
+        self.grad_allreduces += 1
+        outs, i = [], 0
+        for grads, _, _ in parts:
+            out = []
+            for g in grads:
+                if g is None:
+                    out.append(None)
+                    continue
+                n = g.numel()
+                out.append(flat[i:i + n].view_as(g))
+                i += n
+            outs.append(out)
+        return outs
 
     def sum(self, t: torch.Tensor) -> torch.Tensor:
         t = t.clone()
@@ -103,12 +120,16 @@ class SingleProcess:
     """The same interface for one process (no communication)."""
 
     rank, world = 0, 1
+    grad_allreduces = 0
 
     def shard(self, total: int):
         return 0, total
 
     def allreduce_grads(self, grads, count, total):
         return list(grads)
+
+    def allreduce_grads_multi(self, parts):
+        return [list(grads) for grads, _, _ in parts]
 
     def sum(self, t):
         return t

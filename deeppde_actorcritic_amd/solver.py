@@ -126,6 +126,7 @@ class DeepNN(nn.Module):
         return ops.mlp_prepare([g.detach() for g in self.bn_gamma], [bt.detach() for bt in self.bn_beta],
                                [w.detach() for w in self.W], self.b.detach(), self.ekn_head, True)
 
+    @torch.no_grad()
     def mlp_view(self):
         """This network as dpac_rollout_nn_fwd reads it (BN scale = rs * gamma, the same
         product forward() forms)."""
@@ -423,9 +424,14 @@ class _SplitCriticGraphs:
         return list(self.back_out)
 
 
-# DPAC_GBACK=early (default): the critic's G backward starts right after the critic head;
-# "late": after V's update and the actor's BPTT are queued (round-2 order; measurement).
-GBACK = os.environ.get("DPAC_GBACK", "early")
+# DPAC_GBACK=late (default): the critic's G backward is launched on its side stream after V's
+# update and the actor's BPTT are queued, so it runs beside the BPTT and the actor's
+# parameter gradients; "early": right after the critic head, beside V's backward, V's Adam
+# step and the actor's terminal V(x_N) too.  Both measure the same and give
+# bitwise the same parameters (tests/test_gpu_training.py).
+GBACK = os.environ.get("DPAC_GBACK", "late")
+if GBACK not in ("early", "late"):
+    raise ValueError(f"DPAC_GBACK must be 'early' or 'late', got {GBACK!r}")
 
 
 def _huber_grad(delta):
@@ -731,8 +737,11 @@ class ActorCriticSolver(object):
     def train_iteration(self, data_critic, data_actor, total=None):
         """One iteration of solver.py:67-70 (critic step, then actor step).  With HIP
         graphs the actor's forward rollout runs on a side stream during the critic step;
-        under TD1 the critic's G-network backward and G's Adam update run on a second
-        side stream beside the actor's BPTT (which reads V, not G)."""
+        under TD1 the critic's G-network backward runs on a second side stream beside the
+        actor's BPTT (which reads V, not G).  Two gradient all-reduces per iteration (SURVEY
+        §8(e)): V's half of the critic step (the actor's terminal V(x_N) needs the updated V,
+        solver.py:221), then the actor's gradients and G's half in one flattened exchange (G
+        is next read by the following iteration's critic step)."""
         if not self._actor_split_ok():
             self.train_step_critic(data_critic, total)
             self.train_step_actor(data_actor, total)
@@ -766,22 +775,23 @@ class ActorCriticSolver(object):
             if GBACK == "early":  # G's backward beside V's update and the actor's terminal V
                 gG = cg.launch_back(head_done)
             gV = self.par.allreduce_grads(cg.grads_v(), ccnt, ctot)
-            # one Adam step of the critic in two parts: V now (the actor reads it), G beside the BPTT
+            # one Adam step of the critic in two parts: V now (the actor reads it), G after the
+            # actor's exchange (same lr and t: advance=False here)
             self.optimizer_critic.apply_gradients(
                 zip(gV, self.model_critic.NN_value.trainable_variables()), advance=False)
         g = sg.grads()  # the actor's terminal V(x_N), BPTT and parameter gradients
-        if cg is not None:
-            if GBACK != "early":
-                gG = cg.launch_back(head_done)
-            with torch.cuda.stream(cg.side):
-                gG = self.par.allreduce_grads(gG, ccnt, ctot)
-                self.optimizer_critic.apply_gradients(
-                    zip(gG, self.model_critic.NN_value_grad.trainable_variables()))
         cnt = da.x0.shape[0]
-        g = self.par.allreduce_grads(g, cnt, total or cnt * self.par.world)
+        atot = total or cnt * self.par.world
+        if cg is None:
+            g = self.par.allreduce_grads(g, cnt, atot)
+            self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))
+            return
+        if GBACK != "early":
+            gG = cg.launch_back(head_done)
+        torch.cuda.current_stream().wait_stream(cg.side)  # G's gradients, made on the side stream
+        g, gG = self.par.allreduce_grads_multi([(g, cnt, atot), (gG, ccnt, ctot)])
         self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))
-        if cg is not None:
-            torch.cuda.current_stream().wait_stream(cg.side)
+        self.optimizer_critic.apply_gradients(zip(gG, self.model_critic.NN_value_grad.trainable_variables()))
 
     def train_step_actor(self, train_data, total=None):
         g = self._grads("actor", lambda d: self.grad_actor(

@@ -53,8 +53,8 @@ extern "C" {
  * dpac_rollout_nn_mask_bytes.  3: dpac_mlp gains weight_x3 / weight_t_x3 (split-fp16
  * images) and dpac_mlp_prepare writes them.  4: the split-fp16 images are fragment-major
  * (below) and the float fused rollout / BPTT (dpac_rollout_nn_fwd[_masked],
- * dpac_rollout_nn_bwd_masked) read them too.  Bindings must refuse a library of another
- * version. */
+ * dpac_rollout_nn_bwd_masked) read them too.  5: adds dpac_critic_loss_grad.  Bindings must
+ * refuse a library of another version. */
 #define DPAC_ABI_VERSION 5
 
 /* status codes besides hipError_t values */

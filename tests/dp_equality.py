@@ -14,7 +14,8 @@ rows [off, off+cnt) of that batch) and compares every parameter; then train() en
 (validation metrics reduced over ranks, the final arrays gathered in global order) against
 the single-process train().  Cases: lqr_var_d20 (BASELINE configs[3]) and vdp_d20
 (configs[4]) at d = 20 with TD1, lqr_var_d20 with TD2 (no G network: no split critic).
-Writes one JSON object (max relative differences) and exits non-zero past 1e-12.
+Writes one JSON object (max relative differences) and exits non-zero past 1e-12, or if a
+train_iteration issues other than two gradient all-reduces (V's; the actor's with G's).
 With --backend nccl every collective of that path runs on RCCL (the seed broadcast on a
 device tensor, the gradient all-reduces on the current and the side stream, the metric
 reductions, the device all-gather of the final arrays); a one-GPU box runs it as one rank.
@@ -58,10 +59,15 @@ def make(cfg, par):
     return psol.ActorCriticSolver(cfg, bsde, seed=7, sampler="device", parallel=par)
 
 
-def iterate(sp, B, N, k):
-    for _ in range(k):  # solver.train's loop body
+def iterate(sp, B, N, k, counts=None):
+    """k iterations of solver.train's loop body; counts (a list) receives the gradient
+    all-reduces each train_iteration issued (two)."""
+    for _ in range(k):
         dc, da = sp.sample_iteration(B, N, N)
+        before = sp.par.grad_allreduces
         sp.train_iteration(dc, da, B)
+        if counts is not None:
+            counts.append(sp.par.grad_allreduces - before)
         sp.prefetch_samples(B, N, N)
     torch.cuda.synchronize()
     return [v.detach().cpu().clone() for v in sp.critic_variables() + sp.actor_variables()]
@@ -91,10 +97,12 @@ def main():
     B, N = a.batch, 10
     for name, td in CASES:
         cfg = config(name, td, B, N)
-        dp = iterate(make(cfg, DataParallel()), B, N, a.iters)
+        counts = []
+        dp = iterate(make(cfg, DataParallel()), B, N, a.iters, counts)
         cfg2 = config(name, td, B, N)
         hist_dp = make(cfg2, DataParallel()).train()
-        case = {"config": name, "TD": td, "batch": B, "N": N, "iterations": a.iters}
+        case = {"config": name, "TD": td, "batch": B, "N": N, "iterations": a.iters,
+                "grad_allreduces_per_iteration": counts}
         if rank == 0:
             ref = iterate(make(config(name, td, B, N), None), B, N, a.iters)
             case["params_max_rel_diff"] = rel(dp, ref)
@@ -105,7 +113,8 @@ def main():
             case["final_arrays_rows"] = int(hist_dp[1].shape[0])
             case["final_arrays_max_abs_diff"] = max(outs)
             good = (case["params_max_rel_diff"] <= TOL and case["history_max_rel_diff"] <= TOL
-                    and case["final_arrays_max_abs_diff"] <= TOL and case["final_arrays_rows"] == B)
+                    and case["final_arrays_max_abs_diff"] <= TOL and case["final_arrays_rows"] == B
+                    and counts == [2] * a.iters)
             case["ok"] = good
             ok = ok and good
             print(json.dumps(case), flush=True)

@@ -19,13 +19,18 @@ Tolerances (float32 against float64):
     matched trajectories within 1e-5 (1 + |ref|) on x, u and dt;
   * gradients (flipped trajectories removed from both sides): per tensor
     max |g - g_ref| <= 1e-3 * max |g_ref|;
-  * training, lqr_d20 at BASELINE's B = 4096 (6 iterations, validated after every one, against
-    tests/golden/train_lqr_d20_B4096.npz): |err_value - ref| <= 1e-5 and
+  * training (6 iterations, validated after every one) against the committed float64 oracle
+    vectors tests/golden/train_<config>_B<batch>.npz — lqr_d20 and ekn_d20 at B = 4096,
+    lqr_var_d20 at 2048, vdp_d20 at 8192: |err_value - ref| <= 1e-5 and
     |err_control - ref| <= 1e-5 (absolute, relative-L2 units) at every logged step, the
-    losses within 1e-4 relative, and every parameter summary within 2e-4 (1 + |ref|).
+    losses within 1e-4 relative, and every parameter summary within 2e-4 (1 + |ref|);
+  * full-size shards (lqr_var_d20 16384 = 8 x 2048, vdp_d20 65536 = 8 x 8192): finite losses
+    and gradients, and the count-weighted shard gradients sum to the whole batch's within
+    1e-4 of its largest entry per tensor.
 Measured on MI355X (round 3): paths 6.3e-7, gradients 9.6e-5 (critic) / 1.2e-6 (actor),
 err_value 9.1e-7, err_control 4.5e-7, parameters 2.1e-5 (profiles/r03_fp32_parity.txt).
 """
+import glob
 import os
 
 import numpy as np
@@ -42,7 +47,7 @@ from tests.helpers import full_config, rel_close
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_lqr_d20_B4096.npz")
+GOLDENS = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_*_B*.npz")))
 
 TOL_FLIP = 1e-3      # fraction of trajectories allowed to flip an exit decision
 TOL_PATH = 1e-5      # matched trajectories, |a - b| <= TOL_PATH (1 + |b|)
@@ -130,12 +135,13 @@ def _grad_err(gp, go):
     return worst
 
 
-@pytest.mark.parametrize("name,B", [("LQR", 1100), ("LQR_var", 1100), ("EKN", 1040)])
+@pytest.mark.parametrize("name,B", [("LQR", 1100), ("LQR_var", 1100), ("EKN", 1040), ("VDP", 1100)])
 def test_fp32_production_gradients_vs_oracle_tape(name, B):
     """The critic's and the actor's float32 gradients from the production kernels (critic_front +
     critic_G_back: fused TD1 G network; actor_forward + actor_grads_from: 16-row fast path,
     sign-bit-mask BPTT, k-major images, parameter-gradient kernel) against the oracle's
-    GradientTape restatement (float64) on the same batch."""
+    GradientTape restatement (float64) on the same batch.  VDP runs BASELINE configs[4]'s
+    shapes (d = 20, c = 10: actor 20-200-200-200-10, one-lane trajectory groups)."""
     N, T = 50, 0.2
     cfg = full_config(name, 20, N=N, hidden=(200, 200, 200), batch=B, scheme="adaptive", td="TD1",
                       dtype="float32")
@@ -172,17 +178,22 @@ def _summarize(tensors):
     return np.array(out, dtype=np.float64)
 
 
-def test_fp32_production_training_lqr_d20_b4096_vs_oracle_vectors():
-    """BASELINE configs[1] (lqr_d20, TD1, normal sampling, adaptive, B = 4096, 3x200 MLPs)
-    trained in float32 on the production path — HIP graphs, the split critic step with the
-    fused TD1 G network, the actor step on the 16-row fast path with the sign-bit-mask BPTT —
-    from the oracle's initial weights and numpy sample stream, against the float64 oracle's
-    6 iterations (tests/golden/make_train_golden.py)."""
-    g = np.load(GOLDEN)
+@pytest.mark.parametrize("path", GOLDENS, ids=[os.path.basename(p)[6:-4] for p in GOLDENS])
+def test_fp32_production_training_vs_oracle_vectors(path):
+    """A BASELINE config trained in float32 on the production path — HIP graphs, the split
+    critic step with the fused TD1 G network, the actor step on the 16-row fast path with the
+    sign-bit-mask BPTT, split-fp16 MFMA — from the oracle's initial weights and numpy sample
+    stream, against the float64 oracle's iterations (tests/golden/make_train_golden.py):
+    lqr_d20 at B = 4096 (configs[1]), ekn_d20 at 4096 (configs[2]), lqr_var_d20 at 2048 and
+    vdp_d20 at 8192 (the per-rank shards of configs[3] and [4] on 8 GPUs).
+    Reference: solver.py:36-71 (train), :109-119 (err_value / err_control)."""
+    g = np.load(path)
+    name = str(g["name"]) if "name" in g.files else "lqr_d20"
     seed_params, seed_np, iters, batch, valid = (int(v) for v in g["meta"])
-    assert iters >= 5 and batch > 1024
-    cfg = baseline_config(iters, 1, "float32", batch, valid, "lqr_d20")
-    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=seed_params, sampler="host", graphs=True)
+    assert iters >= 4 and batch > 1024
+    cfg = baseline_config(iters, 1, "float32", batch, valid, name)
+    bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
+    sp = psol.ActorCriticSolver(cfg, bsde, seed=seed_params, sampler="host", graphs=True)
     np.random.seed(seed_np)
     hist = sp.train()[0]
     assert sp._actor_split_ok() and sp._critic_split_ok()
@@ -194,8 +205,55 @@ def test_fp32_production_training_lqr_d20_b4096_vs_oracle_vectors():
     d_loss = np.abs(hist[:, 1:3] - ref[:, 1:3]) / (1 + np.abs(ref[:, 1:3]))
     got = _summarize(sp.critic_variables() + sp.actor_variables())
     d_par = np.abs(got - g["params"]) / (1 + np.abs(g["params"]))
-    print(f"\n[fp32 training lqr_d20 B={batch}] max |d err_value| {d_val.max():.2e}, "
+    print(f"\n[fp32 training {name} B={batch}] max |d err_value| {d_val.max():.2e}, "
           f"max |d err_control| {d_ctl.max():.2e}, losses {d_loss.max():.2e}, params {d_par.max():.2e}")
     assert d_val.max() <= TOL_ERR and d_ctl.max() <= TOL_ERR
     assert d_loss.max() <= TOL_LOSS
     assert got.shape == g["params"].shape and d_par.max() <= TOL_PARAM
+
+
+TOL_SHARD = 1e-4  # per tensor, max |sum of weighted shard gradients - whole batch| <= TOL_SHARD max |whole|
+
+
+@pytest.mark.parametrize("name,total,world", [("lqr_var_d20", 16384, 8), ("vdp_d20", 65536, 8)])
+def test_fp32_full_size_shards_sum_to_whole_batch(name, total, world):
+    """BASELINE configs[3] / [4] at full size in float32 on the production kernels: the global
+    batch (16384 / 65536, N = 100, 3x200 MLPs, TD1, adaptive) and its 8 per-rank shards (2048 /
+    8192 trajectories: what each GPU of the 8-GPU run computes; the device sampler keyed by
+    global trajectory index).  Losses and gradients are finite, and the count-weighted sum of
+    the shard gradients (what parallel.DataParallel's all-reduce forms) equals the whole
+    batch's within TOL_SHARD (float32 summation order: chunked row sums per launch).
+    Reference: solver.py:73-83 (batch-mean losses), :85-97 (gradients)."""
+    from deeppde_actorcritic_amd.parallel import shard_range
+    cfg = baseline_config(1, 1, "float32", total, 256, name)
+    bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
+    sp = psol.ActorCriticSolver(cfg, bsde, seed=3, sampler="device", graphs=False)
+    N, key = 100, 0x5EED
+
+    def grads(data):
+        front = sp.critic_front(data)
+        assert len(front) == 6  # fused TD1 critic
+        gc = [g.detach().double() for g in front[0] + sp.critic_G_back(front)]
+        ga = [g.detach().double() for g in sp.actor_grads_from(sp.actor_forward(data))]
+        return gc + ga
+
+    full = bsde.sample_device("normal", total, N, key, 0, torch.float32)
+    with torch.no_grad():
+        lc = float(sp._valid_loss_critic(full, total))
+        la = float(sp._valid_loss_actor(full, total))
+    assert np.isfinite(lc) and np.isfinite(la)
+    g_full = grads(full)
+    assert all(bool(torch.isfinite(g).all()) for g in g_full)
+    g_sum = None
+    for r in range(world):
+        off, cnt = shard_range(total, r, world)
+        shard = bsde.sample_device("normal", cnt, N, key, off, torch.float32)
+        assert torch.equal(shard.x0, full.x0[off:off + cnt])
+        g = grads(shard)
+        assert all(bool(torch.isfinite(t).all()) for t in g)
+        g = [t * (cnt / total) for t in g]
+        g_sum = g if g_sum is None else [a + b for a, b in zip(g_sum, g)]
+    worst = max(float((a - b).abs().max()) / max(float(b.abs().max()), 1e-30) for a, b in zip(g_sum, g_full))
+    print(f"\n[fp32 shards {name} {world}x{total // world}] losses {lc:.4e} {la:.4e}; "
+          f"max rel |sum of shards - whole| {worst:.2e}")
+    assert worst <= TOL_SHARD

@@ -3,14 +3,16 @@
 * Joint actor-critic training of every BASELINE equation at d = 20 (VDP with c = 10) against
   the live oracle, small nets, both the eager path and the production path (HIP graphs, the
   critic step split at the G network, the actor's forward rollout on a side stream).
-* lqr_d20 at BASELINE's batch (B = 4096, N = 100, 3x200 MLPs, TD1, adaptive) against the
-  committed oracle vectors tests/golden/train_lqr_d20_B4096.npz (made by
-  tests/golden/make_train_golden.py; the oracle needs about a CPU-minute per iteration there).
+* the BASELINE configs at their batches (lqr_d20 and ekn_d20 at B = 4096, lqr_var_d20 at 2048,
+  vdp_d20 at 8192; N = 100, 3x200 MLPs, TD1, adaptive) against the committed oracle vectors
+  tests/golden/train_<config>_B<batch>.npz (made by tests/golden/make_train_golden.py in the
+  build container: too slow for a GPU test's time limit).
 Same initial weights (ActorCriticSolver(seed) draws the Keras initialisers from
 torch.Generator().manual_seed(seed), which the oracle's init_params reproduces) and the same
 numpy sample stream (sampler="host").  Tolerance: 1e-8 relative (float64; GEMM and reduction
 re-association only).
 """
+import glob
 import os
 
 import numpy as np
@@ -24,7 +26,7 @@ from oracle import solver as osol
 from tests.helpers import full_config, rel_close
 
 pytestmark = pytest.mark.gpu
-GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_lqr_d20_B4096.npz")
+GOLDENS = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_*_B*.npz")))
 
 
 def pair(cfg, seed, graphs):
@@ -61,12 +63,17 @@ def summarize(tensors):
 
 
 @pytest.mark.parametrize("graphs", [False, True])
-def test_lqr_d20_baseline_batch_matches_oracle_vectors(graphs):
+@pytest.mark.parametrize("path", GOLDENS, ids=[os.path.basename(p)[6:-4] for p in GOLDENS])
+def test_baseline_batch_matches_oracle_vectors(path, graphs):
+    """float64 training at the BASELINE configs' batches against the committed oracle vectors
+    (lqr_d20 / ekn_d20 at 4096, lqr_var_d20 at 2048, vdp_d20 at 8192), 1e-8 relative."""
     from deeppde_actorcritic_amd.config import baseline_config
-    g = np.load(GOLDEN)
+    g = np.load(path)
+    name = str(g["name"]) if "name" in g.files else "lqr_d20"
     seed_params, seed_np, iters, batch, valid = (int(v) for v in g["meta"])
-    cfg = baseline_config(iters, 1, "float64", batch, valid, "lqr_d20")
-    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=seed_params, sampler="host", graphs=graphs)
+    cfg = baseline_config(iters, 1, "float64", batch, valid, name)
+    bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
+    sp = psol.ActorCriticSolver(cfg, bsde, seed=seed_params, sampler="host", graphs=graphs)
     np.random.seed(seed_np)
     hist = sp.train()[0]
     ref = g["history"]
@@ -142,3 +149,26 @@ def test_baseline_config0_float32_matches_oracle():
     print(f"\n[configs[0] fp32] max |d err_value| {dv:.2e}, |d err_control| {dc:.2e}")
     assert dv <= 1e-5 and dc <= 1e-5
     assert rel_close(hp[:, 1:3], ho[:, 1:3], 1e-4)
+
+
+def test_gback_early_and_late_give_bitwise_equal_parameters(monkeypatch):
+    """The critic's G-network backward launched right after the critic head (DPAC_GBACK=early:
+    beside V's backward, V's Adam step, the actor's terminal V and then the BPTT) or after the
+    BPTT is queued (late, the default) must give bitwise the same parameters: it shares no
+    buffer with the work it overlaps (ops._workspace tags 0 / 1).  float32 production path
+    (HIP graphs, split critic / actor steps, device sampler), lqr_d20 shape at B = 2048."""
+    from deeppde_actorcritic_amd.config import baseline_config
+    out = {}
+    for mode in ("early", "late"):
+        monkeypatch.setattr(psol, "GBACK", mode)
+        cfg = baseline_config(4, 10 ** 9, "float32", 2048, 256, "lqr_d20")
+        sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=5, sampler="device")
+        for _ in range(4):
+            dc, da = sp.sample_iteration(2048, 100, 100)
+            sp.train_iteration(dc, da, 2048)
+            sp.prefetch_samples(2048, 100, 100)
+        torch.cuda.synchronize()
+        assert sp._critic_split_ok()
+        out[mode] = [v.detach().cpu().clone() for v in sp.critic_variables() + sp.actor_variables()]
+    for a, b in zip(out["early"], out["late"]):
+        assert torch.equal(a, b)

@@ -139,3 +139,45 @@ def test_gloo_world3_gather_rows_and_seed_broadcast():
     for rank, got, seed in res:
         assert torch.equal(got, full)
         assert seed == 1000
+
+
+def _multi_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        par = DataParallel()
+        gen = torch.Generator().manual_seed(100 + rank)
+        a = [torch.randn(3, 4, generator=gen, dtype=torch.float64), None,
+             torch.randn(5, generator=gen, dtype=torch.float64)]
+        b = [torch.randn(7, generator=gen, dtype=torch.float64)]
+        cnt_a, cnt_b = (3, 5) if rank == 0 else (2, 4)
+        sep = (par.allreduce_grads([t.clone() if t is not None else None for t in a], cnt_a, 5),
+               par.allreduce_grads([t.clone() for t in b], cnt_b, 9))
+        n0 = par.grad_allreduces
+        one = par.allreduce_grads_multi([(a, cnt_a, 5), (b, cnt_b, 9)])
+        q.put((rank, sep, one, par.grad_allreduces - n0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_allreduce_grads_multi_is_one_exchange():
+    """allreduce_grads_multi (the actor's gradients and the critic's G half in one flattened
+    all-reduce, solver.train_iteration) equals one allreduce_grads per part, each with its own
+    shard weight count/total, and counts as ONE gradient all-reduce."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_multi_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, sep, one, n in res:
+        assert n == 1
+        for s_part, o_part in zip(sep, one):
+            for s, o in zip(s_part, o_part):
+                assert (s is None) == (o is None)
+                if s is not None:
+                    assert torch.equal(s, o)
