@@ -17,10 +17,11 @@ comma     := ,
 DIM_LIST  := $(subst $(comma), ,$(DIMS))
 EVEN_LIST := $(subst $(comma), ,$(DIMS_EVEN))
 BASEFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wno-pass-failed \
-             -ffp-contract=off
+             -ffp-contract=off -MMD -MP
 HIPFLAGS  := $(BASEFLAGS) -DDPAC_DIMS=$(DIMS) -DDPAC_DIMS_EVEN=$(DIMS_EVEN)
 EQNS      := lqr lqrvar ekn vdp
-HDRS      := $(wildcard $(CSRC)/*.h) include/dpac.h
+# header dependencies: generated per object (-MMD); a build without .d files rebuilds all
+HDRS      :=
 eqn_dims   = $(if $(filter vdp,$(1)),$(EVEN_LIST),$(DIM_LIST))
 EQN_OBJS  := $(foreach e,$(EQNS),$(foreach d,$(call eqn_dims,$(e)),$(foreach t,f32 f64,$(OBJDIR)/dpac_eqn_$(e)_$(t)_d$(d).o)))
 OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_params.o $(EQN_OBJS)
@@ -49,6 +50,8 @@ $(OBJDIR)/dpac_eqn_$(1)_$(2)_d$(3).o: $(CSRC)/dpac_eqn_$(1).hip $(HDRS)
 	$(HIPCC) $(BASEFLAGS) -DDPAC_DIMS=$(3) -DDPAC_DIMS_EVEN=$(3) -DDPAC_TU_DOUBLE=$(if $(filter f64,$(2)),1,0) -c $$< -o $$@
 endef
 $(foreach e,$(EQNS),$(foreach d,$(call eqn_dims,$(e)),$(foreach t,f32 f64,$(eval $(call EQN_RULE,$(e),$(t),$(d))))))
+
+-include $(OBJS:.o=.d)
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)

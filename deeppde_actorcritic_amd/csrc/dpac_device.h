@@ -112,6 +112,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, kRsrcFlags);
 }
 
+// ---- the split-fp16 range guard (dpac.h dpac_mlp.status) ----
+// An f32 operand a is split as hi = fp16(a), lo = fp16((a - hi) 2^12).  For |a| < 2^15,
+// |hi| <= 2^15 and |a - hi| <= 8 (half an fp16 ulp), so |lo| <= 2^15: both finite.  Past it
+// lo (from 2^15) or hi (from 65520) overflows.
+constexpr float kX3Range = 32768.f;
+// whether any of four split operands lies outside the range (also inf / NaN)
+__device__ __forceinline__ bool x3_bad4(float a, float b, float c, float d) {
+  return !(fabsf(a) < kX3Range) | !(fabsf(b) < kX3Range) | !(fabsf(c) < kX3Range) | !(fabsf(d) < kX3Range);
+}
+__device__ __forceinline__ bool x3_bad(float a) { return !(fabsf(a) < kX3Range); }
+// sticky status word: set (a vector atomic to L2, agent scope) / read at agent scope
+__device__ __forceinline__ void x3_flag(uint32_t* st) {
+  if (st) __hip_atomic_fetch_or(st, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool x3_status_set(const uint32_t* st) {
+  return st && __hip_atomic_load(const_cast<uint32_t*>(st), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+
 // AUX: the cache-policy immediate of the buffer instruction (0 = default; 2 = nt).
 template <int K, int AUX = 0>
 __device__ __forceinline__ void buf_load_dwords(__amdgpu_buffer_rsrc_t r, uint32_t voff,

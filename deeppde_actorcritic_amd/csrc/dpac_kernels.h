@@ -1079,6 +1079,7 @@ NnMlp<T> nn_mlp(const dpac_mlp& h) {
     m.wkm[i] = (const T*)h.weight_km[i];
   }
   m.bias = (const T*)h.bias;
+  m.status = h.status;
   return m;
 }
 
@@ -1258,7 +1259,8 @@ int run_op(const OpArgs& a) {
       r.mb = nn_mask_tile_bytes(m.L);
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
       if constexpr (kFastOk) {  // split-fp16 chain (dpac_rollout_nn_x3.h): needs the forward's mask
-        if (r.mask && bptt_kernel() == 2 &&
+        // (guarded by a status word: only with the f32 fast path's operands for the fallback)
+        if (r.mask && bptt_kernel() == 2 && (!m.status || r.fast) &&
             nn_x3_host(m.L, m.width, (const void* const*)a.mlp.weight_t_x3, m.width[m.L + 1], m.width[0])) {
           for (int i = 0; i <= m.L; ++i) r.wtx3[i] = (const _Float16*)a.mlp.weight_t_x3[i];
           auto kfn = adaptive ? k_rollout_nn_bwd_x3<E, D, DPAC_SCHEME_ADAPTIVE>
@@ -1267,6 +1269,20 @@ int run_op(const OpArgs& a) {
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)NxLds::total))
             return (int)e;
           hipLaunchKernelGGL(kfn, ngrid, nblock, NxLds::total, s, eq, c, m, r);
+          if (m.status) {  // the f32 BPTT, run only once the x3 kernel fell back (dpac.h dpac_mlp.status)
+            int wsum = 0;
+            for (int i = 0; i <= m.L + 1; ++i) wsum += m.width[i];
+            const BwdPlan<T, D, E::CDIM> pl(wsum, m.ztot, true, r.mb);
+            const uint32_t lds = bptt_lds(pl.total, BwdPlan<T, D, E::CDIM>::kMaxDyn);
+            NnBackArgs<T> f = r;
+            f.guard = m.status;
+            auto ffn = adaptive ? k_rollout_nn_bwd2<T, E, D, DPAC_SCHEME_ADAPTIVE, false, true, true>
+                                : k_rollout_nn_bwd2<T, E, D, DPAC_SCHEME_NAIVE, false, true, true>;
+            if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(ffn),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
+              return (int)e;
+            hipLaunchKernelGGL(ffn, ngrid, dim3(kNnBwdThreads), lds, s, eq, c, m, f);
+          }
           break;
         }
       }
@@ -1325,6 +1341,7 @@ int run_op(const OpArgs& a) {
         m.wkm[i] = (const T*)a.mlp.weight_km[i];
       }
       m.bias = (const T*)a.mlp.bias;
+      m.status = a.mlp.status;
       m.fast = nn_fast_host<T>(m.L, m.width, (const void* const*)m.wkm, m.width[0], m.width[m.L + 1]);
       NnRolloutArgs<T> r{};
       r.B = a.B; r.N = a.N; r.cost_order = a.cost_order;
@@ -1359,8 +1376,9 @@ int run_op(const OpArgs& a) {
       }
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
       bool x3 = false;
-      if constexpr (kFastOk)
-        x3 = nn_x3_host(m.L, m.width, (const void* const*)a.mlp.weight_x3, m.width[0], m.width[m.L + 1]);
+      if constexpr (kFastOk)  // guarded by a status word: only with the f32 fast path's operands for the fallback
+        x3 = (!m.status || m.fast) &&
+             nn_x3_host(m.L, m.width, (const void* const*)a.mlp.weight_x3, m.width[0], m.width[m.L + 1]);
       if ((m.fast || x3) && a.save_mask && a.save_z) {  // the 16-row fast paths write the sign bits
         r.save_mask = a.save_mask;
         if (a.mask_written) *a.mask_written = 1;
@@ -1389,7 +1407,8 @@ int run_op(const OpArgs& a) {
 #undef DPAC_NX_SV
 #undef DPAC_NX_LAUNCH
           if (e != hipSuccess) return (int)e;
-          break;
+          if (!m.status) break;
+          r.guard = m.status;  // then the f32 kernel below, run only once the x3 kernel fell back
         }
       }
 #define DPAC_ROLL_NN(SCH, CO)                                                                                   \

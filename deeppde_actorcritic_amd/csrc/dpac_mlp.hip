@@ -200,6 +200,7 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
       const int64_t cap = (((int64_t)1 << 31) - 1) / (max_ld(a) * 4) / kPgxSR * kPgxSR;
       if (a.rows_per_chunk <= cap) {
         a.part = (float*)ws;
+        a.status = net.status;
         const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
         for (int l = 0; l <= a.L; ++l) {
           // layers the split kernel does not cover (a wide layer with more than 13 input
@@ -211,6 +212,17 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
           if (x3ok) e = launch_x3_layer(a, l, nch, s0);
           else e = launch_f32_layer<float>(a, l, nch, s0);
           if (e) return e;
+        }
+        if (net.status) {  // the f32 kernel over every layer, run only once an x3 kernel fell back
+          PgArgs<float> f = a;
+          f.status = nullptr;
+          f.guard = net.status;
+          int hmax = 0;
+          for (int l = 0; l <= a.L; ++l) hmax = std::max(hmax, a.width[l + 1]);
+          hipLaunchKernelGGL((k_param_grads<float, 16, 2, 1>), dim3((unsigned)nch, (unsigned)((hmax + 127) / 128),
+                                                                   (unsigned)(a.L + 1)),
+                             dim3(kPgThreads), 0, s0, f, -1);
+          if (hipError_t e = hipGetLastError()) return (int)e;
         }
         const int64_t n = a.ptot + a.width[a.L + 1];
         hipLaunchKernelGGL(k_param_grads_reduce<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s0,
@@ -334,20 +346,13 @@ int x3_launch(K kfn, const X3Args& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Grid of a guarded f32 fallback launch (dpac.h dpac_mlp.status): a grid-stride pass over
+// every row tile; when the word is clear each workgroup exits after one load.
+constexpr int64_t kFallbackBlocks = 512;
+
 template <typename T>
 int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void* out,
              void* save_z, const TdRows* td, hipStream_t s) {
-  if constexpr (std::is_same<T, float>::value) {
-    if (x3_all(net, net.weight_x3)) {
-      X3Args a = x3_args(net, rows, net.weight_x3, td);
-      if (td) a.gdot = (float*)td->gdot;
-      a.x = (const float*)x;
-      a.ldx = ldx;
-      a.out = (float*)out;
-      a.z = (float*)save_z;
-      return x3_launch(k_mlp_rows_fwd_x3, a, s);
-    }
-  }
   MrArgs<T> a = mr_args<T>(net, rows);
   set_td(a, td);
   if (td) a.gdot = (T*)td->gdot;
@@ -356,8 +361,26 @@ int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void
   a.out = (T*)out;
   a.z = (T*)save_z;
   constexpr int ROWS = MrCfg<T>::RT * 16;
-  hipLaunchKernelGGL(k_mlp_rows_fwd<T>, dim3((unsigned)((rows + ROWS - 1) / ROWS)),
-                     dim3(kMrThreads), 0, s, a);
+  const int64_t nblk = (rows + ROWS - 1) / ROWS;
+  if constexpr (std::is_same<T, float>::value) {
+    // split-fp16 products when the images are given (and, guarded, the f32 operands too)
+    if (x3_all(net, net.weight_x3) && (!net.status || x3_all(net, net.weight))) {
+      X3Args xa = x3_args(net, rows, net.weight_x3, td);
+      if (td) xa.gdot = (float*)td->gdot;
+      xa.x = (const float*)x;
+      xa.ldx = ldx;
+      xa.out = (float*)out;
+      xa.z = (float*)save_z;
+      xa.status = net.status;
+      if (int e = x3_launch(k_mlp_rows_fwd_x3, xa, s)) return e;
+      if (!net.status) return 0;
+      a.guard = net.status;  // the f32 kernel recomputes everything once the x3 kernel fell back
+      hipLaunchKernelGGL(k_mlp_rows_fwd<T>, dim3((unsigned)std::min(nblk, kFallbackBlocks)), dim3(kMrThreads), 0,
+                         s, a);
+      return (int)hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL(k_mlp_rows_fwd<T>, dim3((unsigned)nblk), dim3(kMrThreads), 0, s, a);
   return (int)hipGetLastError();
 }
 
@@ -365,14 +388,29 @@ template <typename T>
 int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const void* save_z,
              const void* g_out, void* G, void* g_x, const TdRows* td, hipStream_t s) {
   if constexpr (std::is_same<T, float>::value) {
-    if (x3_all(net, net.weight_t_x3)) {
+    if (x3_all(net, net.weight_t_x3) && (!net.status || x3_all(net, wt))) {
       X3Args a = x3_args(net, rows, net.weight_t_x3, td);
       if (td) a.g_gdot = (const float*)td->g_gdot;
       a.z = (float*)save_z;
       a.g_out = (const float*)g_out;
       a.G = (float*)G;
       a.g_x = (float*)g_x;
-      return x3_launch(k_mlp_rows_bwd_x3, a, s);
+      a.status = net.status;
+      if (int e = x3_launch(k_mlp_rows_bwd_x3, a, s)) return e;
+      if (!net.status) return 0;
+      MrArgs<T> f = mr_args<T>(net, rows);  // the f32 kernel, run only once the x3 kernel fell back
+      set_td(f, td);
+      if (td) f.g_gdot = (const T*)td->g_gdot;
+      for (int i = 0; i <= f.L; ++i) f.wt[i] = (const T*)wt[i];
+      f.z = (T*)save_z;
+      f.g_out = (const T*)g_out;
+      f.G = (T*)G;
+      f.g_x = (T*)g_x;
+      f.guard = net.status;
+      constexpr int ROWS = MrCfg<T>::RT * 16;
+      hipLaunchKernelGGL(k_mlp_rows_bwd<T>, dim3((unsigned)std::min((rows + ROWS - 1) / ROWS, kFallbackBlocks)),
+                         dim3(kMrThreads), 0, s, f);
+      return (int)hipGetLastError();
     }
   }
   MrArgs<T> a = mr_args<T>(net, rows);

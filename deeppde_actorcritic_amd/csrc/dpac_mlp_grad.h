@@ -53,6 +53,9 @@ struct PgArgs {
   int64_t off_gamma[DPAC_MLP_MAX_HIDDEN + 2], off_beta[DPAC_MLP_MAX_HIDDEN + 2];
   int64_t off_W[DPAC_MLP_MAX_HIDDEN + 1];
   T* part;  // [nchunks][ptot]
+  uint32_t* status;       // split-fp16 kernel: the range guard (dpac.h dpac_mlp.status), or null
+  const uint32_t* guard;  // f32 kernel as the fallback of a split-fp16 launch: run only once this
+                          // word is set, every layer in one launch (blockIdx.z); null = always run
 };
 
 template <typename T>
@@ -82,7 +85,7 @@ struct PgStage {
 // (H <= 32) WI = 4, WJ = 1, so no wavefront multiplies padding columns.
 // NTI / NTJ are compile-time: the MFMA loop is straight-line code.
 template <typename T, int NTI, int NTJ, int WI>
-__global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, const int l) {
+__global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, const int l_arg) {
   using MF = Mfma<T>;
   constexpr int WJ = 4 / WI;
   constexpr int SR = PgCfg<T>::SR;
@@ -95,6 +98,8 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
   constexpr uint32_t ES = sizeof(T);
   __shared__ T sA[SR * LDA];
   __shared__ T sB[SR * LDB];
+  if (a.guard && !x3_status_set(a.guard)) return;  // a fallback launch: only once the x3 kernel fell back
+  const int l = l_arg >= 0 ? l_arg : (int)blockIdx.z;  // l_arg < 0: every layer, one per grid z
   const int grp = blockIdx.y;
   const int K = a.width[l], H = a.width[l + 1];
   const int col0 = grp * CW;

@@ -91,6 +91,8 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
   float* const s_cmax = reinterpret_cast<float*>(smem + kMain);
   float* const s_cfac = s_cmax + 4 * CW;
   int* const s_cexp = reinterpret_cast<int*>(s_cfac + CW);
+  if (x3_status_set(a.status)) return;  // fell back: the f32 kernel after this one does the work
+  bool bad = false;  // a split operand outside the range (dpac.h dpac_mlp.status)
   const int grp = blockIdx.y;
   const int K = a.width[l], H = a.width[l + 1];
   const int col0 = grp * CW;
@@ -190,6 +192,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
       }
       pgh8 h, lo;
       pgx_split8(v, h, lo);
+      bad |= x3_bad4(v[0], v[1], v[2], v[3]) | x3_bad4(v[4], v[5], v[6], v[7]);
       *reinterpret_cast<pgh8*>(sA + ((0 * 4 + rb) * KP + k) * 8) = h;
       *reinterpret_cast<pgh8*>(sA + ((1 * 4 + rb) * KP + k) * 8) = lo;
     }
@@ -226,6 +229,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
       for (int i = 0; i < 8; ++i) vb[q][i] *= sc;
       pgh8 h, lo, h12;
       pgx_split8(vb[q], h, lo);
+      bad |= x3_bad4(vb[q][0], vb[q][1], vb[q][2], vb[q][3]) | x3_bad4(vb[q][4], vb[q][5], vb[q][6], vb[q][7]);
 #pragma unroll
       for (int i = 0; i < 8; ++i) h12[i] = h[i] * (_Float16)kPgxLo;  // exact: |h| < 8
       *reinterpret_cast<pgh8*>(sB + ((0 * 4 + rb) * CW + c) * 8) = h;
@@ -347,6 +351,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
     part[a.off_beta[0] + tid] = sb;
     part[a.off_gamma[0] + tid] = ss;
   }
+  if (bad) x3_flag(a.status);
 }
 
 }  // namespace dpac

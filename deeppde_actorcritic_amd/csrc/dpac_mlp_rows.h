@@ -79,6 +79,9 @@ struct MrArgs {
   T td_sa, td_sb;
   T* gdot;           // forward: [rows] sum_j (sigma_j dw_j) G_j; `out` is not written
   const T* g_gdot;   // backward: [rows]; dL/d out_j = g_gdot * (sigma_j dw_j)
+  // the f32 fallback of a split-fp16 launch (dpac.h dpac_mlp.status): run only once the
+  // word is set, over all row tiles with a grid-stride loop (a small grid); null = always run
+  const uint32_t* guard;
 };
 
 // (sigma(x,u) dw)_j of row r (0 past d).
@@ -415,72 +418,82 @@ template <typename T>
 __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_fwd(const MrArgs<T> a) {
   constexpr int RT = MrCfg<T>::RT, ROWS = RT * 16;
   __shared__ T s_img[2][ROWS * kMrLd];
+  if (a.guard && !x3_status_set(a.guard)) return;  // a fallback launch: only once the x3 kernel fell back
   const int tid = threadIdx.x;
   const int wave = mr_wave(tid), lane = tid % 64;
-  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
-  const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
-  const int d = a.width[0];
-  // a_0 = BN_0(x) into image 0 (solver.py:265); everything else zero
-  for (int e = tid; e < ROWS * kMrLd; e += kMrThreads) {
-    const int r = e / kMrLd, k = e % kMrLd;
-    T v = T(0);
-    if (k < d && r < rows_live) v = a.shift[0][k] + a.x[(row0 + r) * a.ldx + k] * a.scale[0][k];
-    s_img[0][e] = v;
-    s_img[1][e] = T(0);
-  }
-  T td_pre[kTdPre];
-  const bool have_pre = td_prefetch<T, ROWS>(a, row0, rows_live, a.width[a.L + 1], tid, td_pre);
-  __syncthreads();
-  int pq = 0;
-  for (int l = 0; l <= a.L; ++l) {
-    const int Nout = a.width[l + 1];
-    MrFwdEpi<T, RT> epi{a.scale[l + 1], a.shift[l + 1], l == a.L ? a.bias : nullptr, l < a.L,
-                        Nout, rows_live, s_img[pq ^ 1],
-                        a.z ? a.z + row0 * a.ztot + a.zoff[l + 1] : nullptr, a.ztot,
-                        a.gdot ? nullptr : a.out + row0 * Nout, Nout};
-    mr_layer<T, RT>(s_img[pq], a.width[l], Nout, a.weight[l], a.wkm[l], wave, lane, epi);
+  const int64_t nblk = (a.rows + ROWS - 1) / ROWS;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {  // one pass unless a fallback launch
+    if (blk != (int64_t)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+    const int64_t row0 = blk * ROWS;
+    const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
+    const int d = a.width[0];
+    // a_0 = BN_0(x) into image 0 (solver.py:265); everything else zero
+    for (int e = tid; e < ROWS * kMrLd; e += kMrThreads) {
+      const int r = e / kMrLd, k = e % kMrLd;
+      T v = T(0);
+      if (k < d && r < rows_live) v = a.shift[0][k] + a.x[(row0 + r) * a.ldx + k] * a.scale[0][k];
+      s_img[0][e] = v;
+      s_img[1][e] = T(0);
+    }
+    T td_pre[kTdPre];
+    const bool have_pre = td_prefetch<T, ROWS>(a, row0, rows_live, a.width[a.L + 1], tid, td_pre);
     __syncthreads();
-    pq ^= 1;
+    int pq = 0;
+    for (int l = 0; l <= a.L; ++l) {
+      const int Nout = a.width[l + 1];
+      MrFwdEpi<T, RT> epi{a.scale[l + 1], a.shift[l + 1], l == a.L ? a.bias : nullptr, l < a.L,
+                          Nout, rows_live, s_img[pq ^ 1],
+                          a.z ? a.z + row0 * a.ztot + a.zoff[l + 1] : nullptr, a.ztot,
+                          a.gdot ? nullptr : a.out + row0 * Nout, Nout};
+      mr_layer<T, RT>(s_img[pq], a.width[l], Nout, a.weight[l], a.wkm[l], wave, lane, epi);
+      __syncthreads();
+      pq ^= 1;
+    }
+    if (a.gdot) td_dot_rows<T, ROWS>(a, s_img[pq], row0, rows_live, a.width[a.L + 1], tid, have_pre, td_pre);
   }
-  if (a.gdot) td_dot_rows<T, ROWS>(a, s_img[pq], row0, rows_live, a.width[a.L + 1], tid, have_pre, td_pre);
 }
 
 template <typename T>
 __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_bwd(const MrArgs<T> a) {
   constexpr int RT = MrCfg<T>::RT, ROWS = RT * 16;
   __shared__ T s_img[2][ROWS * kMrLd];
+  if (a.guard && !x3_status_set(a.guard)) return;  // a fallback launch: only once the x3 kernel fell back
   const int tid = threadIdx.x;
   const int wave = mr_wave(tid), lane = tid % 64;
-  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
-  const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
   const int L = a.L, hout = a.width[L + 1];
-  // G_{L+1} = dL/d out: into image 0 and to G
-  for (int e = tid; e < ROWS * kMrLd; e += kMrThreads) {
-    const int r = e / kMrLd, k = e % kMrLd;
-    T v = T(0);
-    if (k < hout && r < rows_live) {
-      v = a.g_gdot ? a.g_gdot[row0 + r] * td_sdw(a, row0 + r, k, hout)  // td_assemble_bwd's product
-                   : a.g_out[(row0 + r) * hout + k];
-      a.G[(row0 + r) * a.gtot + a.goff[L + 1] + k] = v;
+  const int64_t nblk = (a.rows + ROWS - 1) / ROWS;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {  // one pass unless a fallback launch
+    if (blk != (int64_t)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+    const int64_t row0 = blk * ROWS;
+    const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
+    // G_{L+1} = dL/d out: into image 0 and to G
+    for (int e = tid; e < ROWS * kMrLd; e += kMrThreads) {
+      const int r = e / kMrLd, k = e % kMrLd;
+      T v = T(0);
+      if (k < hout && r < rows_live) {
+        v = a.g_gdot ? a.g_gdot[row0 + r] * td_sdw(a, row0 + r, k, hout)  // td_assemble_bwd's product
+                     : a.g_out[(row0 + r) * hout + k];
+        a.G[(row0 + r) * a.gtot + a.goff[L + 1] + k] = v;
+      }
+      s_img[0][e] = v;
+      s_img[1][e] = T(0);
     }
-    s_img[0][e] = v;
-    s_img[1][e] = T(0);
-  }
-  __syncthreads();
-  int pq = 0;
-  for (int l = L; l >= 0; --l) {
-    MrBwdEpi<T, RT> epi{l >= 1 ? a.scale[l] : nullptr, l >= 1 ? a.shift[l] : nullptr,
-                        a.z + row0 * a.ztot + a.zoff[l], a.ztot, a.width[l], rows_live,
-                        s_img[pq ^ 1], a.G + row0 * a.gtot + a.goff[l], a.gtot};
-    mr_layer<T, RT>(s_img[pq], a.width[l + 1], a.width[l], a.wt[l], a.wkm[l], wave, lane, epi);
     __syncthreads();
-    pq ^= 1;
-  }
-  if (a.g_x) {  // dL/dx = G_0 * s_0 (a_0 = beta_0 + x * s_0)
-    const int d = a.width[0];
-    for (int e = tid; e < rows_live * d; e += kMrThreads) {
-      const int r = e / d, k = e % d;
-      a.g_x[(row0 + r) * d + k] = s_img[pq][r * kMrLd + k] * a.scale[0][k];
+    int pq = 0;
+    for (int l = L; l >= 0; --l) {
+      MrBwdEpi<T, RT> epi{l >= 1 ? a.scale[l] : nullptr, l >= 1 ? a.shift[l] : nullptr,
+                          a.z + row0 * a.ztot + a.zoff[l], a.ztot, a.width[l], rows_live,
+                          s_img[pq ^ 1], a.G + row0 * a.gtot + a.goff[l], a.gtot};
+      mr_layer<T, RT>(s_img[pq], a.width[l + 1], a.width[l], a.wt[l], a.wkm[l], wave, lane, epi);
+      __syncthreads();
+      pq ^= 1;
+    }
+    if (a.g_x) {  // dL/dx = G_0 * s_0 (a_0 = beta_0 + x * s_0)
+      const int d = a.width[0];
+      for (int e = tid; e < rows_live * d; e += kMrThreads) {
+        const int r = e / d, k = e % d;
+        a.g_x[(row0 + r) * d + k] = s_img[pq][r * kMrLd + k] * a.scale[0][k];
+      }
     }
   }
 }

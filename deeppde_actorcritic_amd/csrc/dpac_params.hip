@@ -19,6 +19,7 @@
 #include <algorithm>
 
 #include "dpac.h"
+#include "dpac_device.h"
 
 namespace dpac {
 
@@ -110,6 +111,7 @@ struct PrepArgs {
   T gscale;
   T *scales, *wt, *km, *tkm;
   _Float16 *x3, *tx3;                     // split-fp16 images (float only)
+  uint32_t* status;                       // the range guard (dpac.h dpac_mlp.status), or null
 };
 
 __device__ __forceinline__ int k16(int k) { return (k + 15) / 16 * 16; }
@@ -130,6 +132,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> 
   const int64_t nx = a.x3 ? a.xoff[a.L + 1] : 0;
   const int64_t ny = a.tx3 ? a.yoff[a.L + 1] : 0;
   const int64_t n4 = ns + nw + nk + nt;
+  bool bad = false;  // a split-fp16 image value outside the split range
   for (int64_t e = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; e < n4 + nx + ny;
        e += (int64_t)gridDim.x * kAdamThreads) {
     if (e >= n4) {  // split-fp16 images, fragment-major: [tile][chunk][hi|lo][lane][8] halves per layer
@@ -150,6 +153,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> 
         v = fwd ? (float)a.W[i][(int64_t)k * a.width[i + 1] + n]
                 : (float)(a.W[i][(int64_t)n * K + k] * (a.gscale * a.gamma[i + 1][k]));
       (fwd ? a.x3 : a.tx3)[f] = x3_part(v, part);
+      bad |= x3_bad(v);
       continue;
     }
     if (e < ns) {
@@ -183,6 +187,7 @@ __global__ __launch_bounds__(kAdamThreads) void k_mlp_prepare(const PrepArgs<T> 
       a.tkm[f] = k < K ? a.W[i][n * K + k] * (a.gscale * a.gamma[i + 1][k]) : T(0);
     }
   }
+  if (bad) x3_flag(a.status);
 }
 
 template <typename T>
@@ -219,6 +224,7 @@ int prepare(const dpac_mlp& net, double gscale, void* scales, void* wt, void* km
   a.yoff[a.L + 1] = yo;
   a.x3 = (_Float16*)x3;
   a.tx3 = (_Float16*)tx3;
+  a.status = (x3 || tx3) ? net.status : nullptr;
   a.gscale = (T)gscale;
   a.scales = (T*)scales;
   a.wt = (T*)wt;

@@ -79,6 +79,7 @@ struct NnMlp {
   const T* bias;
   int fast;  // the actor-shape fast path applies (nn_fast_host)
   const _Float16* wx3[DPAC_MLP_MAX_HIDDEN + 1];  // split-fp16 images of weight (k_rollout_nn_x3)
+  uint32_t* status;  // the split-fp16 range guard (dpac.h dpac_mlp.status), or null
 };
 
 template <typename T>
@@ -91,6 +92,8 @@ struct NnRolloutArgs {
   uint8_t* save_mask;   // optional (fast path only): the hidden activations' sign bits,
                         // [N][ceil(B/16)][mb] bytes (FwdEpiM's layout per 16-row tile)
   int mb;               // mask bytes per 16-row tile
+  const uint32_t* guard;  // the f32 fallback of a split-fp16 launch: run only once this word
+                          // is set (dpac.h dpac_mlp.status); null = always run
 };
 
 // out[16 x Nout] = in[16 x K] @ W[K x Nout] for the workgroup's 16 rows, this
@@ -874,6 +877,7 @@ struct NnBackArgs {
   const uint8_t* mask;  // optional (fast path): the forward's sign bits, [N][ceil(B/16)][mb]
   int mb;
   const _Float16* wtx3[DPAC_MLP_MAX_HIDDEN + 1];  // split-fp16 images of wt (k_rollout_nn_bwd_x3)
+  const uint32_t* guard;  // as NnRolloutArgs::guard
 };
 
 // The actor's BPTT through a fused NN rollout, as one launch: the reverse time
@@ -1001,6 +1005,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn(const E eq, const Dev
   using TR = Transition<T, E, SCHEME>;
   __shared__ T s_x0[kNnRows * kNnLd];   // BN_0(x_t)
   __shared__ T s_pq[2][kNnRows * kNnLd];
+  if (a.guard && !x3_status_set(a.guard)) return;  // a fallback launch: only once the x3 kernel fell back
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
   const int64_t row0 = (int64_t)blockIdx.x * kNnRows;

@@ -249,6 +249,7 @@ __global__ __launch_bounds__(kNnBwdThreads) void k_rollout_nn_bwd2(const E eq, c
   using PL = BwdPlan<T, D, CD>;
   __shared__ T s_pq[2][kNnRows * kNnLd];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  if (a.guard && !x3_status_set(a.guard)) return;  // a fallback launch: only once the x3 kernel fell back
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
   const bool stager = wave == kNnWaves && !(DPAC_BWD2_ABLATE & 1);

@@ -82,8 +82,9 @@ __device__ __forceinline__ nxf4 nx_mma(nxh8 a, nxh8 b, nxf4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// four consecutive features f0..f0+3 (f0 % 4 == 0) of one row, split, as two 8-byte LDS writes
-__device__ __forceinline__ void nx_put4(_Float16* img, int ld, int row, int f0, nxf4 v) {
+// four consecutive features f0..f0+3 (f0 % 4 == 0) of one row, split, as two 8-byte LDS writes;
+// true if one of them is outside the split range (dpac.h dpac_mlp.status)
+__device__ __forceinline__ bool nx_put4(_Float16* img, int ld, int row, int f0, nxf4 v) {
   nxh4 h, l;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -93,13 +94,15 @@ __device__ __forceinline__ void nx_put4(_Float16* img, int ld, int row, int f0, 
   _Float16* p = img + row * ld + (f0 >> 5) * 64 + (f0 & 31);
   *reinterpret_cast<nxh4*>(p) = h;
   *reinterpret_cast<nxh4*>(p + 32) = l;
+  return x3_bad4(v[0], v[1], v[2], v[3]);
 }
 
-__device__ __forceinline__ void nx_put1(_Float16* img, int ld, int row, int col, float v) {
+__device__ __forceinline__ bool nx_put1(_Float16* img, int ld, int row, int col, float v) {
   const _Float16 h = (_Float16)v;
   _Float16* p = img + row * ld + (col >> 5) * 64 + (col & 31);
   p[0] = h;
   p[32] = (_Float16)((v - (float)h) * kNxLo);
+  return x3_bad(v);
 }
 
 // A operands of chunks [c0, c0 + NC) of the feature tiles tA, tB of a fragment-major split-fp16
@@ -215,12 +218,14 @@ __device__ __forceinline__ int nx_mask_idx(int lane) {  // byte of the tile this
 
 // Forward epilogue of a hidden layer (pre-BN z of hidden layer h): save z, BN, the sign bit,
 // y + relu(y) split into the next image, the mask byte.  bn: LDS [scale | shift] of layer h,
-// zero past Nout.  Tiles past the layer are skipped (wave-uniform).
+// zero past Nout.  Tiles past the layer are skipped (wave-uniform).  Returns whether a split
+// operand left the range.
 template <bool SAVE, bool MASK>
-__device__ __forceinline__ void nx_fwd_epi(const nxf4 (&acc)[2][3], int wave, int lane, int Nout, const float* bn,
+__device__ __forceinline__ bool nx_fwd_epi(const nxf4 (&acc)[2][3], int wave, int lane, int Nout, const float* bn,
                                            _Float16* out, float* zrow0, int ztot, bool zvec, int rows_live,
                                            uint8_t* mtile) {
   const int row = lane & 15;
+  bool bad = false;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int tl = wave + 8 * j;
@@ -247,20 +252,23 @@ __device__ __forceinline__ void nx_fwd_epi(const nxf4 (&acc)[2][3], int wave, in
       nib |= (e < nv && y[e] > 0.f) ? 1u << e : 0u;
       y[e] = e < nv ? y[e] + fmaxf(y[e], 0.f) : 0.f;  // y + relu(y) (solver.py:269)
     }
-    nx_put4(out, kNxLd, row, f0, y);
+    bad |= nx_put4(out, kNxLd, row, f0, y);
     if constexpr (MASK && !(DPAC_NX_ABLATE & 2)) {
       const uint32_t w = nx_quad_gather(nib, lane);
       mtile[64 * tl + nx_mask_idx(lane)] = (uint8_t)nx_pick4(w, lane & 3);
     }
   }
+  return bad;
 }
 
 // BPTT epilogue of hidden layer h: the activation factor 1 + [y_h > 0] from the forward's
 // mask bytes, G_h = v * 2^(e-1) (the row's scale undone) to global, v split into the next image.
-__device__ __forceinline__ void nx_bwd_epi(const nxf4 (&acc)[2][3], int wave, int lane, int Nout,
+// Returns whether a split operand left the range.
+__device__ __forceinline__ bool nx_bwd_epi(const nxf4 (&acc)[2][3], int wave, int lane, int Nout,
                                            const uint32_t (&mb)[2], _Float16* out, float* grow0, int gtot,
                                            bool gvec, int rows_live, float ri) {
   const int row = lane & 15, i = lane & 3;
+  bool bad = false;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int tl = wave + 8 * j;
@@ -282,8 +290,9 @@ __device__ __forceinline__ void nx_bwd_epi(const nxf4 (&acc)[2][3], int wave, in
           if (e < nv) gp[e] = gv[e];
       }
     }
-    nx_put4(out, kNxLd, row, f0, v);
+    bad |= nx_put4(out, kNxLd, row, f0, v);
   }
+  return bad;
 }
 
 __device__ __forceinline__ void nx_lds_zero(unsigned char* lds, uint32_t bytes, int tid, int nthreads) {
@@ -333,6 +342,8 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
   float* const part = reinterpret_cast<float*>(nx_lds + NxLds::part);
   float* const s_bn = reinterpret_cast<float*>(nx_lds + NxLds::bn);
   auto img = [&](int i) { return (i & 1) ? img1 : img0; };
+  if (x3_status_set(mlp.status)) return;  // fell back: the f32 kernel after this one does the work
+  bool bad = false;                       // a split operand outside the range (dpac.h dpac_mlp.status)
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
   const int64_t row0 = (int64_t)blockIdx.x * kNnRows;
@@ -392,7 +403,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
     if (stepper) {
 #pragma unroll
       for (int m = 0; m < M; ++m)
-        if (own.valid(m)) nx_put1(in0, kNxLd0, g, own.j(m), b0[m] + xv[m] * s0[m]);
+        if (own.valid(m)) bad |= nx_put1(in0, kNxLd0, g, own.j(m), b0[m] + xv[m] * s0[m]);
     }
   };
   T x[M];
@@ -413,7 +424,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
     {  // hidden layer 1 from a0 (narrow K, resident weights)
       nxf4 acc[2][3];
       nx_prod<1, kNxLd0, 0>(in0, 0, rih, ril, acc, lane);
-      nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[1], s_bn, img(0),
+      bad |= nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[1], s_bn, img(0),
                              SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[1] : nullptr, mlp.ztot, zvec, rows_live,
                              mt);
     }
@@ -430,7 +441,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
 #endif
       const int ln = l + 1 < L ? l + 1 : 1;  // the next wide layer (this step's or the next one's first)
       nx_loadw<kNxRing>(wh, wl, mlp.wx3[ln], mlp.width[ln + 1], kNxWide, 0, wave, wave + 8, lane);
-      nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[l + 1], s_bn + l * kNxBnLd, img(l),
+      bad |= nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[l + 1], s_bn + l * kNxBnLd, img(l),
                              SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[l + 1] : nullptr, mlp.ztot, zvec,
                              rows_live, MASK ? mt + 13 * 64 * l : nullptr);
       NN_MARK(t, 1 + 2 * l);
@@ -509,6 +520,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
       a.disc[lc.b] = disc;
     }
   }
+  if (bad) x3_flag(mlp.status);
 }
 
 // ---------------------------------------------------------------------------
@@ -531,6 +543,8 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
   float* const part = reinterpret_cast<float*>(nx_lds + NxLds::part);
   float* const s_rinv = reinterpret_cast<float*>(nx_lds + NxLds::rinv);
   auto img = [&](int i) { return (i & 1) ? img1 : img0; };
+  if (x3_status_set(mlp.status)) return;  // fell back: the f32 kernel after this one does the work
+  bool bad = false;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
   const int64_t row0 = (int64_t)blockIdx.x * kNnRows;
@@ -658,11 +672,11 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
 #pragma unroll
       for (int m = 0; m < MC; ++m)
         if (ownu.valid(m)) {
-          nx_put1(in0, kNxLd0, g, ownu.j(m), gu[m] * sc);
+          bad |= nx_put1(in0, kNxLd0, g, ownu.j(m), gu[m] * sc);
           if (live) grow[ownu.j(m)] = gu[m];
         }
       if (mlp.ekn && lc.p == 0) {
-        nx_put1(in0, kNxLd0, g, CD, goc * sc);
+        bad |= nx_put1(in0, kNxLd0, g, CD, goc * sc);
         if (live) grow[CD] = goc;
       }
       if (lc.p == 0) s_rinv[g] = ldexpf(1.f, ex - 1);
@@ -674,8 +688,8 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
     {  // hidden layer L from the output's gradient (narrow K, resident weights)
       nxf4 acc[2][3];
       nx_prod<1, kNxLd0, 0>(in0, 0, rih, ril, acc, lane);
-      nx_bwd_epi(acc, wave, lane, mlp.width[L], mb[L - 1], img(0), a.G + (rowt + row0) * a.gtot + a.goff[L],
-                 a.gtot, gvec, rows_live, ri);
+      bad |= nx_bwd_epi(acc, wave, lane, mlp.width[L], mb[L - 1], img(0), a.G + (rowt + row0) * a.gtot + a.goff[L],
+                        a.gtot, gvec, rows_live, ri);
     }
     NN_MARK(t, 3);
     __syncthreads();
@@ -690,8 +704,8 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
 #endif
       const int ln = l - 1 >= 1 ? l - 1 : L - 1;  // the next wide layer (this step's or the next one's first)
       nx_loadw<kNxRing>(wh, wl, a.wtx3[ln], mlp.width[ln], kNxWide, 0, wave, wave + 8, lane);
-      nx_bwd_epi(acc, wave, lane, mlp.width[l], mb[l - 1], img(L - l), a.G + (rowt + row0) * a.gtot + a.goff[l],
-                 a.gtot, gvec, rows_live, ri);
+      bad |= nx_bwd_epi(acc, wave, lane, mlp.width[l], mb[l - 1], img(L - l), a.G + (rowt + row0) * a.gtot + a.goff[l],
+                        a.gtot, gvec, rows_live, ri);
       NN_MARK(t, 3 + 2 * (L - l));
       __syncthreads();
       NN_MARK(t, 4 + 2 * (L - l));
@@ -724,4 +738,5 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
     NN_MARK(t, 13);
   }
   if (a.g_x0 && live) own.store(a.g_x0 + lc.b * D, lam);
+  if (bad) x3_flag(mlp.status);
 }

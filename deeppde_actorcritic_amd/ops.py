@@ -115,7 +115,7 @@ class MlpView:
     contiguous, on the GPU, in the rollout's dtype."""
 
     def __init__(self, scales, shifts, weights, bias, ekn_head: bool, weights_km=None,
-                 weights_x3=None, weights_t_x3=None):
+                 weights_x3=None, weights_t_x3=None, status=None):
         L = len(weights) - 1
         if not 1 <= L <= _lib.MLP_MAX_HIDDEN:
             raise ValueError(f"the fused rollout supports 1..{_lib.MLP_MAX_HIDDEN} hidden layers, got {L}")
@@ -142,6 +142,9 @@ class MlpView:
                 self.halves += list(imgs)  # alive here, outside the same-dtype `tensors`
                 for i, w in enumerate(imgs):
                     getattr(m, slot)[i] = w.data_ptr()
+        self.status = status  # the split-fp16 range guard word (dpac_mlp.status), or None
+        if status is not None:
+            m.status = status.data_ptr()
         self.struct = m
         self.widths = [m.width[i] for i in range(L + 2)]
 
@@ -162,6 +165,39 @@ WEIGHT_KM = os.environ.get("DPAC_WEIGHT_KM", "on")
 MLP_MATH = os.environ.get("DPAC_MLP_MATH", "x3")
 if MLP_MATH not in ("x3", "f32"):
     raise ValueError(f"DPAC_MLP_MATH must be 'x3' or 'f32', got {MLP_MATH!r}")
+
+
+# The split-fp16 range guard (dpac.h dpac_mlp.status): every float view with split-fp16
+# images carries its device's status word, so an operand outside the split range (|a| >= 2^15,
+# inf, NaN) makes that launch, and every later one on the device, run the exact-f32 kernels.
+# DPAC_X3_GUARD=0 passes no word (the unguarded kernels; timing comparisons only).
+X3_GUARD = os.environ.get("DPAC_X3_GUARD", "1") != "0"
+_X3_STATUS = {}
+
+
+def x3_status(device) -> torch.Tensor:
+    """The device's split-fp16 status word (int32 [1], sticky; never freed: captured HIP graphs
+    keep its address)."""
+    device = torch.device(device)
+    key = (device.type, device.index if device.index is not None else torch.cuda.current_device())
+    st = _X3_STATUS.get(key)
+    if st is None:
+        st = _X3_STATUS[key] = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", key[1]))
+    return st
+
+
+def x3_fell_back(device="cuda") -> bool:
+    """Whether a split-fp16 launch on `device` met an operand outside the split range (its
+    launches, and every later one, then ran on the exact-f32 kernels).  Synchronises."""
+    return bool(int(x3_status(device).item()) & _lib.X3_FELL_BACK)
+
+
+def x3_status_reset(device="cuda") -> None:
+    """Clear the device's status word: the split-fp16 kernels run again.  Synchronises the device
+    first: no guarded launch may be in flight (dpac.h)."""
+    torch.cuda.synchronize(device)
+    x3_status(device).zero_()
+    torch.cuda.synchronize(device)
 
 
 def _x3_halves(k, n):
@@ -186,10 +222,11 @@ def mlp_prepare(gam, bet, Ws, b, ekn: bool, want_wt: bool, want_km: bool = True)
     _require_gpu(*gam, *Ws)
     widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
     L1 = len(Ws)
-    raw = MlpView(gam, bet, Ws, b, ekn)  # bn_scale slots point at the raw gammas
     kw = dict(dtype=ref.dtype, device=ref.device)
     km = want_km and WEIGHT_KM == "on" and ref.dtype == torch.float32
     x3 = MLP_MATH == "x3" and ref.dtype == torch.float32
+    status = x3_status(ref.device) if (x3 and X3_GUARD) else None
+    raw = MlpView(gam, bet, Ws, b, ekn, status=status)  # bn_scale slots point at the raw gammas
     S = torch.empty(sum(widths), **kw)
     nw = [widths[i] * widths[i + 1] for i in range(L1)]
     nk = [widths[i + 1] * _k16(widths[i]) for i in range(L1)]
@@ -211,7 +248,7 @@ def mlp_prepare(gam, bet, Ws, b, ekn: bool, want_wt: bool, want_km: bool = True)
     km_f = split(KM, nk, [(widths[i + 1], _k16(widths[i])) for i in range(L1)]) if km else None
     x3_f = split(X3, nx, [(nx[i],) for i in range(L1)]) if X3 is not None else None
     x3_b = split(TX3, ny, [(ny[i],) for i in range(L1)]) if TX3 is not None else None
-    view = MlpView(list(torch.split(S, widths)), bet, Ws, b, ekn, km_f, x3_f, x3_b)
+    view = MlpView(list(torch.split(S, widths)), bet, Ws, b, ekn, km_f, x3_f, x3_b, status)
     wt = split(WT, nw, [(widths[i + 1], widths[i]) for i in range(L1)]) if want_wt else None
     wt_km = split(TKM, nt, [(widths[i], _k16(widths[i + 1])) for i in range(L1)]) \
         if TKM is not None else None

@@ -53,9 +53,10 @@ extern "C" {
  * dpac_rollout_nn_mask_bytes.  3: dpac_mlp gains weight_x3 / weight_t_x3 (split-fp16
  * images) and dpac_mlp_prepare writes them.  4: the split-fp16 images are fragment-major
  * (below) and the float fused rollout / BPTT (dpac_rollout_nn_fwd[_masked],
- * dpac_rollout_nn_bwd_masked) read them too.  5: adds dpac_critic_loss_grad.  Bindings must
- * refuse a library of another version. */
-#define DPAC_ABI_VERSION 5
+ * dpac_rollout_nn_bwd_masked) read them too.  5: adds dpac_critic_loss_grad.  6: dpac_mlp gains
+ * `status` (the split-fp16 range guard, below).  Bindings must refuse a library of another
+ * version. */
+#define DPAC_ABI_VERSION 6
 
 /* status codes besides hipError_t values */
 #define DPAC_OK 0
@@ -265,7 +266,21 @@ int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
  *     width[i] / width[i+1] (backward): [ceil(cols / 16)][ceil(K / 32)][2][64][8] halves,
  *     element [t][c][p][l][e] = part p (0 hi, 1 lo) of the operand at column
  *     n = 16 t + (l % 16), k = 32 c + 8 (l / 16) + e, zero where n >= cols or k >= K.
- *     Operand range: |activations| and the per-row scaled gradients below 65504.
+ *     Operand range: an operand is split exactly only while |a| < 2^15 (hi and the 2^12-scaled
+ *     lo both finite fp16 numbers); see `status`.
+ *   status (optional, float split-fp16 only; NULL = unguarded): a device word, the range
+ *     guard of the split-fp16 products.  Every split-fp16 kernel checks each operand it splits
+ *     (activations, the backward chain's scaled gradients, the parameter gradients' A rows) and
+ *     dpac_mlp_prepare checks the weight images it writes; an operand with !(|a| < 2^15) (so
+ *     also inf / NaN) sets bit 0 (DPAC_X3_FELL_BACK).  Each split-fp16 launch is followed on
+ *     the same stream by the exact-f32 kernel of the same operation, which runs only when the
+ *     word is set (it then rewrites every output; a split-fp16 kernel that finds the word set
+ *     at its start does no work), so no split-fp16 entry point returns a value the f32 kernels
+ *     would not.  The word is sticky: once set, every later guarded launch with it runs on
+ *     f32.  The caller clears it (zero) only while no guarded launch that uses it is in flight.
+ *     The f32 fallback needs the f32 operands of the direction: weight and weight_km (forward
+ *     entry points), weight_t and weight_t_km (backward entry points); without them the
+ *     split-fp16 kernels are not used when a status word is given.
  * 1 <= n_hidden <= DPAC_MLP_MAX_HIDDEN, every width <= DPAC_MLP_MAX_WIDTH.
  * Outputs as dpac_rollout_fwd, with u [N][B][c] the control actually applied.
  * y/disc (optional, both or neither): the pathwise cost in `cost_order`.
@@ -286,7 +301,9 @@ typedef struct dpac_mlp {
   const void* weight_km[DPAC_MLP_MAX_HIDDEN + 1];
   const void* weight_x3[DPAC_MLP_MAX_HIDDEN + 1];
   const void* weight_t_x3[DPAC_MLP_MAX_HIDDEN + 1];
+  uint32_t* status; /* the split-fp16 range guard (above); NULL = unguarded */
 } dpac_mlp;
+#define DPAC_X3_FELL_BACK 1u /* status bit: an operand left the split-fp16 range */
 
 int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
                         int64_t num_sample, int32_t num_steps, double total_time,
@@ -425,7 +442,9 @@ int dpac_mlp_param_grads(int32_t dtype, int64_t rows, const dpac_mlp* net, doubl
  * concatenated over i in dpac_mlp.weight_x3's layout: weight_x3 = [W_i: ceil(width[i+1]/16)
  * x ceil(width[i]/32) x 1024 halves] and weight_t_x3 = [(W_i ⊙ s_{i+1})^T: ceil(width[i]/16)
  * x ceil(width[i+1]/32) x 1024 halves].
- * bn_shift, bias, net->weight_km and the x3 slots of net are not read. */
+ * bn_shift, bias, net->weight_km and the x3 slots of net are not read.  With net->status set, a
+ * split-fp16 image value outside the split range (|v| >= 2^15, inf, NaN) sets DPAC_X3_FELL_BACK
+ * in it. */
 int dpac_mlp_prepare(int32_t dtype, const dpac_mlp* net, double gamma_scale, void* scales,
                      void* weight_t, void* weight_km, void* weight_t_km, void* weight_x3,
                      void* weight_t_x3, void* stream);
