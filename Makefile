@@ -27,7 +27,7 @@ EQN_OBJS  := $(foreach e,$(EQNS),$(foreach d,$(call eqn_dims,$(e)),$(foreach t,f
 OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_params.o $(EQN_OBJS)
 LIB       := $(PKG)/libdpac.so
 
-.PHONY: all lib clean
+.PHONY: all lib ext clean
 all: lib
 lib: $(LIB)
 
@@ -56,8 +56,32 @@ $(foreach e,$(EQNS),$(foreach d,$(call eqn_dims,$(e)),$(foreach t,f32 f64,$(eval
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
+# Dimension plugins: the equation kernels for state dimensions outside DIMS, one shared
+# object per dimension, $(PKG)/libdpac_d<D>.so, linked against libdpac.so; _lib.load() loads
+# every plugin beside libdpac.so, and its instantiations register into the same dispatch table
+# (Registrar, dpac_kernels.h).  VDP needs an even dimension (d = 2c).
+#   make ext EXT_DIMS=7,12
+EXT_DIMS  ?= 7
+EXT_LIST  := $(subst $(comma), ,$(EXT_DIMS))
+EXTDIR    := build/ext
+ext_eqns   = lqr lqrvar ekn $(if $(filter 0,$(shell echo $$(($(1) % 2)))),vdp,)
+ext_objs   = $(foreach e,$(call ext_eqns,$(1)),$(foreach t,f32 f64,$(EXTDIR)/dpac_eqn_$(e)_$(t)_d$(1).o))
+define EXT_RULE
+$(EXTDIR)/dpac_eqn_$(1)_$(2)_d$(3).o: $(CSRC)/dpac_eqn_$(1).hip
+	@mkdir -p $(EXTDIR)
+	$(HIPCC) $(BASEFLAGS) -DDPAC_DIMS=$(3) -DDPAC_DIMS_EVEN=$(3) -DDPAC_TU_DOUBLE=$(if $(filter f64,$(2)),1,0) -c $$< -o $$@
+endef
+$(foreach d,$(EXT_LIST),$(foreach e,$(call ext_eqns,$(d)),$(foreach t,f32 f64,$(eval $(call EXT_RULE,$(e),$(t),$(d))))))
+define EXT_LIB
+$(PKG)/libdpac_d$(1).so: $(call ext_objs,$(1)) $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $$@ $(call ext_objs,$(1)) -L$(PKG) -ldpac -Wl,-rpath,'$$$$ORIGIN'
+endef
+$(foreach d,$(EXT_LIST),$(eval $(call EXT_LIB,$(d))))
+-include $(wildcard $(EXTDIR)/*.d)
+ext: $(foreach d,$(EXT_LIST),$(PKG)/libdpac_d$(d).so)
+
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(PKG)/libdpac_d*.so
 
 # Host-side sanitizer run of the C-ABI validation layer (no GPU needed): every TU with
 # AddressSanitizer + UndefinedBehaviorSanitizer on the host side only (device code is

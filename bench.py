@@ -60,18 +60,19 @@ def barrier(world):
 
 def time_launches(launch, steps, warmup, world):
     """Warm up, then time exactly `steps` back-to-back launches between
-    barrier+synchronize pairs.  A HIP event pair on the launch stream (torch's
-    current stream, which every launch here uses) brackets the same launches:
-    per-launch time = event span / steps, i.e. kernel time plus the dispatch gap
-    between consecutive launches (rocprofv3's per-kernel average excludes it)."""
+    barrier+synchronize pairs (the wall clock: `value` and the headline roofline).  A HIP
+    event pair on the launch stream (torch's current stream, which every launch here uses)
+    brackets the same launches, its start recorded before the wall bracket opens (so the
+    bracket holds nothing but the launches): per-launch time = event span / steps, kernel
+    time plus the dispatch gaps (rocprofv3's per-kernel average excludes them)."""
     for i in range(warmup):
         launch(i)
     torch.cuda.synchronize()
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()  # before the wall bracket: the bracket holds only the K launches (and end's record)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    start.record()
     for i in range(steps):
         launch(i)
     end.record()

@@ -164,8 +164,40 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.argtypes = argtypes
             fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        for path in dim_plugins():
+            try:  # its instantiations register into libdpac's dispatch table as it loads
+                _plugins.append(ctypes.CDLL(path))
+            except OSError as e:  # pragma: no cover - depends on the host
+                _load_error = f"failed to load the dimension plugin {path}: {e}"
+                raise DpacUnavailable(_load_error) from e
         _lib = lib
         return lib
+
+
+_plugins = []
+
+
+def dim_plugins():
+    """The dimension plugins beside libdpac.so (libdpac_d<D>.so, `make ext EXT_DIMS=...`): the
+    equation kernels compiled for state dimensions outside the main build's (4, 5, 10, 20)."""
+    d = os.path.dirname(LIB_PATH)
+    return sorted(os.path.join(d, f) for f in os.listdir(d)
+                  if f.startswith("libdpac_d") and f.endswith(".so"))
+
+
+def build_dim_plugin(*dims) -> None:
+    """Compile and load the dimension plugins for `dims` (hipcc; a few minutes per dimension),
+    e.g. for a config whose dim has no kernel instantiation (DPAC_EUNSUP)."""
+    import subprocess
+    root = os.path.dirname(_HERE)
+    subprocess.run(["make", "-C", root, "-j8", "ext", "EXT_DIMS=" + ",".join(str(int(d)) for d in dims)],
+                   check=True)
+    lib = load()
+    have = {os.path.realpath(p._name) for p in _plugins}
+    for path in dim_plugins():
+        if os.path.realpath(path) not in have:
+            _plugins.append(ctypes.CDLL(path))
+    return lib
 
 
 def call(name: str, *args) -> None:
@@ -174,7 +206,11 @@ def call(name: str, *args) -> None:
     rc = getattr(lib, name)(*args)
     if rc != DPAC_OK:
         msg = lib.dpac_last_error()
-        raise DpacError(name, rc, msg.decode() if msg else "")
+        text = msg.decode() if msg else ""
+        if rc == DPAC_EUNSUP and "no kernel instantiation for dim" in text:
+            text += (" (build a dimension plugin: `make ext EXT_DIMS=<dim>` or "
+                     "deeppde_actorcritic_amd._lib.build_dim_plugin(<dim>))")
+        raise DpacError(name, rc, text)
 
 
 def exported_symbols() -> list:

@@ -155,36 +155,53 @@ inline bool pg_x3(const dpac_mlp& net) {
   return true;
 }
 
+// one split-fp16 launch (dynamic LDS: the plan's size)
+template <int NTI, int NTJ, int WI, bool L0, int NW = kPgxWaves>
+int pgx_launch(const PgArgs<float>& a, int l, dim3 grid, hipStream_t s) {
+  using PL = PgxPlan<NTI, NTJ, WI, L0, NW>;
+  auto k = k_param_grads_x3<NTI, NTJ, WI, L0, NW>;
+  if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, PL::kSmem))
+    return (int)e;
+  hipLaunchKernelGGL(k, grid, dim3(PL::kThreads), PL::kSmem, s, a, l);
+  return (int)hipGetLastError();
+}
+
+// Wide hidden layers (K and H both > 32): two 128-column groups of 8 wavefronts, each staging
+// A (default), or with DPAC_PGX_NW=16 one 256-column group of 16 wavefronts staging A once per
+// chunk (round 4 experiment: at 13 input tiles its 128-register budget spills 87 registers).
+inline bool pgx_wide16() {
+  const char* e = getenv("DPAC_PGX_NW");  // read per launch
+  return e && e[0] == '1' && e[1] == '6';
+}
+
 // one layer of the split-fp16 kernel: wide outputs 1 x 8 waves (one column tile each,
-// 128-column groups: two column tiles per wave, one 256-column group, measured 292 bytes of
-// spills at 13 input tiles), outputs of <= 32 columns 8 x 1 waves over the row tiles
+// 128-column groups; see pgx_wide16), outputs of <= 32 columns 8 x 1 waves over the row tiles
 int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   const int K = a.width[l], H = a.width[l + 1];
   const int nti = (K + 15) / 16;
   if (H <= 32) {
     const int ntj = (H + 15) / 16, nt8 = (nti + 7) / 8;
     const dim3 grid((unsigned)nch, 1u);
-#define DPAC_PGX(NI, NJ) hipLaunchKernelGGL((k_param_grads_x3<NI, NJ, 8, false>), grid, dim3(kPgxThreads), 0, s, a, l)
-    if (nt8 <= 1) {
-      if (ntj == 1) DPAC_PGX(1, 1); else DPAC_PGX(1, 2);
-    } else {
-      if (ntj == 1) DPAC_PGX(2, 1); else DPAC_PGX(2, 2);
-    }
-#undef DPAC_PGX
-  } else {
-    const dim3 grid((unsigned)nch, (unsigned)((H + 127) / 128));
-#define DPAC_PGX(NI, L0) hipLaunchKernelGGL((k_param_grads_x3<NI, 1, 1, L0>), grid, dim3(kPgxThreads), 0, s, a, l)
-    if (l == 0) {  // the input layer (d <= 32: launch() sends the others to the f32 kernel)
-      if (nti <= 1) DPAC_PGX(1, true);
-      else DPAC_PGX(2, true);
-    } else if (nti <= 1) DPAC_PGX(1, false);
-    else if (nti <= 2) DPAC_PGX(2, false);
-    else if (nti <= 4) DPAC_PGX(4, false);
-    else if (nti <= 8) DPAC_PGX(8, false);
-    else DPAC_PGX(13, false);
-#undef DPAC_PGX
+    if (nt8 <= 1) return ntj == 1 ? pgx_launch<1, 1, 8, false>(a, l, grid, s) : pgx_launch<1, 2, 8, false>(a, l, grid, s);
+    return ntj == 1 ? pgx_launch<2, 1, 8, false>(a, l, grid, s) : pgx_launch<2, 2, 8, false>(a, l, grid, s);
   }
-  return (int)hipGetLastError();
+  if (l == 0) {  // the input layer (d <= 32: launch() sends the others to the f32 kernel)
+    const dim3 grid((unsigned)nch, (unsigned)((H + 127) / 128));
+    return nti <= 1 ? pgx_launch<1, 1, 1, true>(a, l, grid, s) : pgx_launch<2, 1, 1, true>(a, l, grid, s);
+  }
+  if (pgx_wide16()) {
+    const dim3 grid((unsigned)nch, (unsigned)((H + 255) / 256));
+    if (nti <= 4) return pgx_launch<4, 1, 1, false, 16>(a, l, grid, s);
+    if (nti <= 8) return pgx_launch<8, 1, 1, false, 16>(a, l, grid, s);
+    return pgx_launch<13, 1, 1, false, 16>(a, l, grid, s);
+  }
+  const dim3 grid((unsigned)nch, (unsigned)((H + 127) / 128));
+  if (nti <= 1) return pgx_launch<1, 1, 1, false>(a, l, grid, s);
+  if (nti <= 2) return pgx_launch<2, 1, 1, false>(a, l, grid, s);
+  if (nti <= 4) return pgx_launch<4, 1, 1, false>(a, l, grid, s);
+  if (nti <= 8) return pgx_launch<8, 1, 1, false>(a, l, grid, s);
+  return pgx_launch<13, 1, 1, false>(a, l, grid, s);
 }
 
 template <typename T>

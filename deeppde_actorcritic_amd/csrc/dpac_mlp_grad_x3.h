@@ -68,24 +68,36 @@ __device__ __forceinline__ void pgx_split8(const float (&v)[8], pgh8& h, pgh8& l
   }
 }
 
-template <int NTI, int NTJ, int WI, bool L0>
-__global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<float> a, const int l) {
-  constexpr int WJ = kPgxWaves / WI;
-  constexpr int CW = 16 * NTJ * WJ;                     // B columns per workgroup (<= 256)
-  constexpr int KP = 16 * NTI * WI;                     // staged A features
-  constexpr int QA = (KP + 127) / 128;                  // A features per staging thread
-  constexpr int QB = (CW + 127) / 128;                  // B columns per staging thread
-  static_assert(CW <= 256 && KP <= DPAC_MLP_MAX_WIDTH, "staging map: 256 columns, 256 features");
+// The layout of one workgroup of NW wavefronts (8: 512 threads; 16: 1024 threads, one 256-column
+// group for the wide layers, so their A operand is staged once per chunk instead of once per
+// 128-column group).  Shared with the host (dynamic LDS size).
+template <int NTI, int NTJ, int WI, bool L0, int NW>
+struct PgxPlan {
+  static constexpr int kThreads = 64 * NW;
+  static constexpr int FL = kThreads / 4;               // staging threads per 8-row block
+  static constexpr int WJ = NW / WI;
+  static constexpr int CW = 16 * NTJ * WJ;             // B columns per workgroup (<= 256)
+  static constexpr int KP = 16 * NTI * WI;             // staged A features
+  static constexpr int QA = (KP + FL - 1) / FL;        // A features per staging thread
+  static constexpr int QB = (CW + FL - 1) / FL;        // B columns per staging thread
   // LDS: the images, halves A [2 parts][4 row blocks][KP][8], B [3][4][CW][8] (hi, lo,
-  // 2^12 hi); after the
-  // row loop the same bytes hold the BN column sums' reduction ([4 rb][2][CW] floats for
-  // the B side, then [4 rb][2][128 QA] for BN_0 on the input layer)
-  constexpr int kImgBytes = (2 * KP + 3 * CW) * 4 * 8 * 2;
-  constexpr int kRedFloats = 4 * 2 * CW + (L0 ? 4 * 2 * 128 * QA : 0);
-  constexpr int kMain = kImgBytes > kRedFloats * 4 ? kImgBytes : kRedFloats * 4;
-  // then the column scaling: sub-chunk maxima [4 rb][CW], rescale factors [CW], exponents [CW]
-  constexpr int kSmem = kMain + (4 * CW + 2 * CW) * 4;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kSmem];
+  // 2^12 hi); after the row loop the same bytes hold the BN column sums' reduction ([4 rb][2][CW]
+  // floats for the B side, then [4 rb][2][FL QA] for BN_0 on the input layer); then the column
+  // scaling: sub-chunk maxima [4 rb][CW], rescale factors [CW], exponents [CW]
+  static constexpr int kImgBytes = (2 * KP + 3 * CW) * 4 * 8 * 2;
+  static constexpr int kRedFloats = 4 * 2 * CW + (L0 ? 4 * 2 * FL * QA : 0);
+  static constexpr int kMain = kImgBytes > kRedFloats * 4 ? kImgBytes : kRedFloats * 4;
+  static constexpr int kSmem = kMain + (4 * CW + 2 * CW) * 4;
+};
+
+template <int NTI, int NTJ, int WI, bool L0, int NW = kPgxWaves>
+__global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> a, const int l) {
+  using PL = PgxPlan<NTI, NTJ, WI, L0, NW>;
+  constexpr int WJ = PL::WJ, CW = PL::CW, KP = PL::KP, QA = PL::QA, QB = PL::QB, FL = PL::FL;
+  static_assert(CW <= 256 && KP <= DPAC_MLP_MAX_WIDTH, "staging map: 256 columns, 256 features");
+  static_assert(CW <= PL::kThreads, "one thread per column in the BN sums' reduction");
+  constexpr int kMain = PL::kMain;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // PL::kSmem bytes (dynamic)
   _Float16* const sA = reinterpret_cast<_Float16*>(smem);
   _Float16* const sB = sA + 2 * 4 * KP * 8;
   float* const s_cmax = reinterpret_cast<float*>(smem + kMain);
@@ -100,7 +112,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = wave / WJ, wj = wave % WJ;
-  const int rb = tid >> 7, fl = tid & 127;
+  const int rb = tid / FL, fl = tid % FL;
   const int64_t chunk = blockIdx.x;
   const int64_t r_begin = chunk * a.rows_per_chunk;
   const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
@@ -117,7 +129,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
   uint32_t offA[QA], offG0[QA];
 #pragma unroll
   for (int q = 0; q < QA; ++q) {
-    const int k = fl + 128 * q;
+    const int k = fl + FL * q;
     const bool v = k < K;
     sa[q] = v ? a.scale[l][k] : 0.f;
     ha[q] = v ? a.shift[l][k] : 0.f;
@@ -129,7 +141,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
   int cexp[QB];  // the columns' running exponents (B staging threads)
 #pragma unroll
   for (int q = 0; q < QB; ++q) {
-    const int c = fl + 128 * q, hcol = col0 + c;
+    const int c = fl + FL * q, hcol = col0 + c;
     const bool bv = c < CW && hcol < H;
     sbv[q] = bv ? a.scale[l + 1][hcol] : 0.f;
     bbv[q] = (bv && last) ? a.bias[hcol] : 0.f;
@@ -177,8 +189,8 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
     __syncthreads();  // the previous sub-chunk's fragment reads are done
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int k = fl + 128 * q;
-      if (k >= KP) continue;  // compile-time for q = 0 when KP >= 128
+      const int k = fl + FL * q;
+      if (k >= KP) continue;  // compile-time for q = 0 when KP >= FL
       float v[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -199,8 +211,8 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
     float vb[QB][8];
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int c = fl + 128 * q;
-      if (c >= CW) continue;  // compile-time for q = 0 when CW >= 128
+      const int c = fl + FL * q;
+      if (c >= CW) continue;  // compile-time for q = 0 when CW >= FL
       float m = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -215,7 +227,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
     __syncthreads();  // the column maxima of the sub-chunk
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int c = fl + 128 * q;
+      const int c = fl + FL * q;
       if (c >= CW) continue;
       const float m = fmaxf(fmaxf(s_cmax[c], s_cmax[CW + c]), fmaxf(s_cmax[2 * CW + c], s_cmax[3 * CW + c]));
       int e = cexp[q];
@@ -315,7 +327,7 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
   float* red0 = red + 4 * 2 * CW;
 #pragma unroll
   for (int q = 0; q < QB; ++q) {
-    const int c = fl + 128 * q;
+    const int c = fl + FL * q;
     if (c < CW) {
       red[(rb * 2 + 0) * CW + c] = csb_b[q];
       red[(rb * 2 + 1) * CW + c] = csb_s[q];
@@ -325,8 +337,8 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
     if (first) {
 #pragma unroll
       for (int q = 0; q < QA; ++q) {
-        red0[(rb * 2 + 0) * 128 * QA + fl + 128 * q] = cs0_b[q];
-        red0[(rb * 2 + 1) * 128 * QA + fl + 128 * q] = cs0_s[q];
+        red0[(rb * 2 + 0) * FL * QA + fl + FL * q] = cs0_b[q];
+        red0[(rb * 2 + 1) * FL * QA + fl + FL * q] = cs0_s[q];
       }
     }
   }
@@ -341,12 +353,12 @@ __global__ __launch_bounds__(kPgxThreads) void k_param_grads_x3(const PgArgs<flo
     part[a.off_beta[l + 1] + col0 + tid] = sb;
     part[a.off_gamma[l + 1] + col0 + tid] = ss;
   }
-  if (L0 && first && tid < K && tid < 128 * QA) {
+  if (L0 && first && tid < K && tid < FL * QA) {
     float sb = 0.f, ss = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      sb += red0[(w * 2 + 0) * 128 * QA + tid];
-      ss += red0[(w * 2 + 1) * 128 * QA + tid];
+      sb += red0[(w * 2 + 0) * FL * QA + tid];
+      ss += red0[(w * 2 + 1) * FL * QA + tid];
     }
     part[a.off_beta[0] + tid] = sb;
     part[a.off_gamma[0] + tid] = ss;

@@ -150,10 +150,7 @@ __device__ __forceinline__ x3f4 x3_load4(__amdgpu_buffer_rsrc_t r, const float* 
 // = ceil(K / 32) as a template constant (straight-line code, counted waits) or 0
 // (runtime K, single-buffered).  epi.pre<NT>() runs before the K loop, epi.post<NT>()
 // after it.  Returns whether a stored operand left the split range (epi.store's result).
-// MIDBAR: a workgroup barrier between the K loop (after epi.post) and the stores, so the
-// epilogue may overwrite the input image `in` (the row-contiguous staging of z / G, below);
-// x3_layer then gives every wave, with or without tiles, exactly one such barrier.
-template <int NT, int NCH, bool MIDBAR, class EPI>
+template <int NT, int NCH, class EPI>
 __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, const _Float16* Wx3, int wave,
                                            int lane, EPI& epi) {
   const int col_l = lane & 15, q = lane >> 4;
@@ -248,7 +245,6 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
   __builtin_amdgcn_sched_barrier(0);
   X3_MARK(epi.mark);
   epi.template post<NT>(wave, lane);
-  if constexpr (MIDBAR) __syncthreads();  // every wave's reads of `in` are done
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < NT; ++j)
@@ -257,7 +253,7 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
   return bad;
 }
 
-template <bool MIDBAR = false, class EPI>
+template <class EPI>
 __device__ __forceinline__ bool x3_layer(const _Float16* in, int K, int Nout, const _Float16* Wx3, int wave,
                                          int lane, EPI& epi) {
   const int ntiles = (Nout + 15) / 16;
@@ -265,45 +261,17 @@ __device__ __forceinline__ bool x3_layer(const _Float16* in, int K, int Nout, co
   const int nch = x3_chunks(K);
   // straight-line layers for the shipped shapes (d <= 32: one chunk; 193..224 wide: seven)
   if (nch == 1) {
-    if (mine == 1) return x3_layer_t<1, 1, MIDBAR>(in, K, Nout, Wx3, wave, lane, epi);
-    if (mine == 2) return x3_layer_t<2, 1, MIDBAR>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 1) return x3_layer_t<1, 1>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 2) return x3_layer_t<2, 1>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (nch == 7) {
-    if (mine == 1) return x3_layer_t<1, 7, MIDBAR>(in, K, Nout, Wx3, wave, lane, epi);
-    if (mine == 2) return x3_layer_t<2, 7, MIDBAR>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 1) return x3_layer_t<1, 7>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 2) return x3_layer_t<2, 7>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (mine == 1) {
-    return x3_layer_t<1, 0, MIDBAR>(in, K, Nout, Wx3, wave, lane, epi);
+    return x3_layer_t<1, 0>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (mine == 2) {
-    return x3_layer_t<2, 0, MIDBAR>(in, K, Nout, Wx3, wave, lane, epi);
+    return x3_layer_t<2, 0>(in, K, Nout, Wx3, wave, lane, epi);
   }
-  if constexpr (MIDBAR) __syncthreads();  // a wave without tiles still meets the barrier
   return false;
-}
-
-// Row-contiguous stores of a hidden layer's z saves / G (round 4).  The epilogue lanes hold
-// four features of one row each, so a wave's direct 16-byte stores cover 16 rows x 64 bytes:
-// half lines, which cost 2.4x the bytes in HBM writes (profiles/r03_pmc_mlp.json).  Instead
-// the epilogue writes its f32 values into the layer's input image (free after the MIDBAR
-// barrier) as [64 rows][kX3StgLd] floats, and after the layer's closing barrier the workgroup
-// writes each row's block as contiguous 16-byte pieces (x3_flush_rows).  The values are the
-// same f32 bits.
-constexpr int kX3StgLd = DPAC_MLP_MAX_WIDTH + 4;  // floats per staged row
-static_assert(kX3Rows * kX3StgLd * 4 <= kX3Rows * kX3Ld * 2, "a staged f32 block fits in one split image");
-
-__device__ __forceinline__ void x3_stage4(float* stg, int row, int f0, x3f4 v) {
-  *reinterpret_cast<x3f4*>(stg + row * kX3StgLd + f0) = v;
-}
-
-// rows [0, rows_live) x features [0, width) of the staged block -> dst (row stride ld floats)
-__device__ __forceinline__ void x3_flush_rows(const float* stg, int width, float* dst, int64_t ld, int rows_live,
-                                              int tid) {
-  const int q4 = (width + 3) >> 2;  // 16-byte pieces per row
-  const __amdgpu_buffer_rsrc_t r = make_rsrc(dst, (uint32_t)(rows_live > 0 ? ((rows_live - 1) * ld + width) * 4 : 0));
-  for (int e = tid; e < kX3Rows * q4; e += kX3Threads) {
-    const int row = e / q4, f0 = (e - row * q4) * 4;
-    if (row >= rows_live) break;
-    const x3f4 v = *reinterpret_cast<const x3f4*>(stg + row * kX3StgLd + f0);
-    x3_store4(r, dst, (uint32_t)(row * ld + f0), width - f0, true, v);
-  }
 }
 
 struct X3Args {
@@ -352,7 +320,6 @@ struct X3FwdEpi {
   int z_ld;                  // floats
   __amdgpu_buffer_rsrc_t ro; // out: the workgroup's rows
   float *zp, *op;            // the same rows as plain pointers (x3_store4's partial quads)
-  float* stg;                // hidden: the z saves staged here (x3_flush_rows), or null: stored directly
   x3f4 s[kX3MaxNT], sh[kX3MaxNT], bb[kX3MaxNT];
   template <int NT>
   __device__ __forceinline__ void pre(int wave, int lane) {
@@ -373,10 +340,7 @@ struct X3FwdEpi {
   __device__ __forceinline__ bool store(int j, int rt, x3f4 zv, int wave, int lane) {
     const int f0 = x3_f0(wave, j, lane), nv = x3_nvalid(f0, Nout);
     const int row = rt * 16 + (lane & 15);
-    if (save) {
-      if (stg) x3_stage4(stg, row, f0, zv);
-      else x3_store4(rz, zp, (uint32_t)(row * z_ld + f0), nv, row < rows_live, zv);
-    }
+    if (save) x3_store4(rz, zp, (uint32_t)(row * z_ld + f0), nv, row < rows_live, zv);
     x3f4 y = zv;
     if (MODE != kX3Hidden) y = y + bb[j];  // addmm(b, y, W) (solver.py:270)
     y = sh[j] + y * s[j];                  // addcmul(beta, y, gamma/sqrt(1+eps))
@@ -414,7 +378,6 @@ struct X3BwdEpi {
   const float* rinv;           // LDS: 2^-e of each row (undoes the chain's row scale)
   const float* zp;             // plain pointers to the same rows (partial quads)
   float *gp, *xp;
-  float* stg;                  // l >= 1: G_l staged here (x3_flush_rows), or null: stored directly
   x3f4 s[kX3MaxNT], sh[kX3MaxNT];
   float ri[kX3RT];
   x3f4 zz[kX3MaxNT][kX3RT];    // z_l of the lane's quads, loaded in post()
@@ -455,8 +418,7 @@ struct X3BwdEpi {
       for (int e = 0; e < 4; ++e) v[e] = v[e] * (y[e] > 0.f ? 2.f : 1.f);  // d(y + relu(y))/dy
     }
     const x3f4 vt = v * ri[rt];                  // exact: a power of two
-    if (stg) x3_stage4(stg, row, f0, vt);
-    else x3_store4(rg, gp, (uint32_t)(row * g_ld + f0), nv, row < rows_live, vt);
+    x3_store4(rg, gp, (uint32_t)(row * g_ld + f0), nv, row < rows_live, vt);
     if (FIRST && gx) x3_store4(rx, xp, (uint32_t)(row * Nout + f0), nv, row < rows_live, vt * s[j]);  // G_0 * s_0
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = e < nv ? v[e] : 0.f;
@@ -530,29 +492,18 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
     const __amdgpu_buffer_rsrc_t rz = x3_rows_rsrc(a.z ? a.z + a.zoff[l + 1] : nullptr, row0, rows_live, a.ztot);
     float* zp = a.z ? a.z + a.zoff[l + 1] + row0 * a.ztot : nullptr;
     if (l < a.L) {
-      float* stg = a.z ? reinterpret_cast<float*>(img(pq)) : nullptr;  // z staged in the free input image
       X3FwdEpi<kX3Hidden> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], nullptr, rows_live, Nout, img(pq ^ 1),
-                              nullptr, rz, a.z != nullptr, a.ztot, make_rsrc(nullptr, 0), zp, nullptr, stg};
-      if (stg) {
-        bad |= x3_layer<true>(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
-        __syncthreads();
-        x3_flush_rows(stg, Nout, zp, a.ztot, rows_live, tid);
-        X3_MARK(3 + 2 * l);
-        pq ^= 1;
-        continue;  // the next layer's barrier orders these LDS reads before its writes
-      }
+                              nullptr, rz, a.z != nullptr, a.ztot, make_rsrc(nullptr, 0), zp, nullptr};
       bad |= x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     } else if (a.gdot) {
       X3FwdEpi<kX3Stage> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], a.bias, rows_live, Nout, nullptr,
                              reinterpret_cast<float*>(img(pq ^ 1)), rz, a.z != nullptr, a.ztot, make_rsrc(nullptr, 0),
-                             zp, nullptr, nullptr};
-      // it writes the free image, which the previous layer's staged z may still be read from
-      if (a.z) bad |= x3_layer<true>(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
-      else x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
+                             zp, nullptr};
+      x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     } else {
       X3FwdEpi<kX3Out> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], a.bias, rows_live, Nout, nullptr, nullptr,
                            rz, a.z != nullptr, a.ztot, x3_rows_rsrc(a.out, row0, rows_live, Nout), zp,
-                           a.out + row0 * Nout, nullptr};
+                           a.out + row0 * Nout};
       x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     }
     __syncthreads();
@@ -619,24 +570,16 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
   for (int l = L; l >= 0; --l) {
     const __amdgpu_buffer_rsrc_t rg = x3_rows_rsrc(a.G + a.goff[l], row0, rows_live, a.gtot);
     float* gp = a.G + a.goff[l] + row0 * a.gtot;
-    if (l >= 1) {  // G_l staged in the free input image, then written row-contiguous
-      float* stg = reinterpret_cast<float*>(img(pq));
+    if (l >= 1) {
       X3BwdEpi<false> epi{2 + 2 * (L - l), a.scale[l], a.shift[l], rows_live, a.width[l], img(pq ^ 1),
                           x3_rows_rsrc(a.z + a.zoff[l], row0, rows_live, a.ztot), a.ztot, rg, a.gtot,
-                          make_rsrc(nullptr, 0), false, nullptr, rinv, a.z + a.zoff[l] + row0 * a.ztot, gp, nullptr,
-                          stg};
-      bad |= x3_layer<true>(img(pq), a.width[l + 1], a.width[l], a.wx3[l], wave, lane, epi);
-      __syncthreads();
-      x3_flush_rows(stg, a.width[l], gp, a.gtot, rows_live, tid);
-      X3_MARK(3 + 2 * (L - l));
-      pq ^= 1;
-      continue;  // the next layer's mid barrier orders these LDS reads before its writes
+                          make_rsrc(nullptr, 0), false, nullptr, rinv, a.z + a.zoff[l] + row0 * a.ztot, gp, nullptr};
+      bad |= x3_layer(img(pq), a.width[l + 1], a.width[l], a.wx3[l], wave, lane, epi);
     } else {
       X3BwdEpi<true> epi{2 + 2 * L, nullptr, nullptr, rows_live, a.width[0], img(pq ^ 1), make_rsrc(nullptr, 0), 0, rg, a.gtot,
                          x3_rows_rsrc(a.g_x, row0, rows_live, a.width[0]), a.g_x != nullptr, a.scale[0], rinv,
-                         nullptr, gp, a.g_x ? a.g_x + row0 * a.width[0] : nullptr, nullptr};
-      // mid barrier: its epilogue writes the image layer 1's staged G is flushed from
-      x3_layer<true>(img(pq), a.width[1], a.width[0], a.wx3[0], wave, lane, epi);  // dL/dx: not split again
+                         nullptr, gp, a.g_x ? a.g_x + row0 * a.width[0] : nullptr};
+      x3_layer(img(pq), a.width[1], a.width[0], a.wx3[0], wave, lane, epi);  // dL/dx: not split again
     }
     __syncthreads();
     X3_MARK(3 + 2 * (L - l));

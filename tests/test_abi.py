@@ -77,7 +77,8 @@ def test_supported_dims():
     assert lib.dpac_supported(ctypes.byref(_params(_lib.EQN_VDP, 20, 10))) == 1
     assert lib.dpac_supported(ctypes.byref(_params(_lib.EQN_VDP, 20, 20))) == 0  # needs d == 2c
     assert lib.dpac_supported(ctypes.byref(_params(_lib.EQN_LQR, 20, 10))) == 0  # needs c == d
-    assert lib.dpac_supported(ctypes.byref(_params(dim=7, cdim=7))) == 0         # not compiled
+    assert lib.dpac_supported(ctypes.byref(_params(dim=7, cdim=7))) == 1         # the d = 7 plugin
+    assert lib.dpac_supported(ctypes.byref(_params(dim=9, cdim=9))) == 0         # not compiled
     bad = _params()
     bad.eqn = 9
     assert lib.dpac_supported(ctypes.byref(bad)) == 0
@@ -143,7 +144,7 @@ def test_validation_without_gpu():
 
 
 def test_unsupported_dim_is_eunsup():
-    p = _params(dim=7, cdim=7)
+    p = _params(dim=9, cdim=9)  # neither the main build (4, 5, 10, 20) nor a plugin (7)
     d = ctypes.c_void_p(0x1000)
     with pytest.raises(_lib.DpacError) as ei:
         _lib.call("dpac_flag_init", ctypes.byref(p), 1, 0, 16, 10, 0.2, d, d, None)
@@ -222,3 +223,20 @@ def test_abi_version_mismatch_is_refused(tmp_path):
     out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
                          env=dict(os.environ, DPAC_LIB=str(so)))
     assert "REFUSED" in out.stdout and "DPAC_ABI_VERSION 1" in out.stdout, out.stdout + out.stderr
+
+
+def test_dimension_plugin_registers_d7():
+    """libdpac_d7.so (make ext, built by __graft_entry__.build()) adds the d = 7 kernels to the
+    dispatch table as _lib.load() loads it; a dimension with neither the main build nor a plugin
+    is reported as DPAC_EUNSUP with the remedy in the message (host-side, no GPU)."""
+    from deeppde_actorcritic_amd import equation as peq
+    from tests.helpers import full_config
+    lib = _lib.load()
+    assert any(p.endswith("libdpac_d7.so") for p in _lib.dim_plugins())
+    for name in ("LQR", "EKN", "LQR_var"):
+        assert lib.dpac_supported(getattr(peq, name)(full_config(name, 7).eqn_config).params()) == 1
+    p9 = peq.LQR(full_config("LQR", 9).eqn_config).params()
+    assert lib.dpac_supported(p9) == 0
+    with pytest.raises(_lib.DpacError) as ei:
+        _lib.call("dpac_flag_init", ctypes.byref(p9), _lib.SCHEME_ADAPTIVE, _lib.F64, 4, 10, 0.2, None, None, None)
+    assert ei.value.code == _lib.DPAC_EUNSUP and "make ext" in str(ei.value)
