@@ -175,11 +175,40 @@ inline bool pgx_wide16() {
   return e && e[0] == '1' && e[1] == '6';
 }
 
-// one layer of the split-fp16 kernel: wide outputs 1 x 8 waves (one column tile each,
-// 128-column groups; see pgx_wide16), outputs of <= 32 columns 8 x 1 waves over the row tiles
+// The merged-group kernel for a wide hidden layer (k_param_grads_x3w: A read once per chunk):
+// rows of z_l and z_{l+1} move by 16-byte LDS-DMA, so every row start must be 16-byte aligned.
+// DPAC_PGX_W=0 selects the two-group kernel (timing comparisons, tests).
+inline bool pgx_w_ok(const PgArgs<float>& a, int l) {
+  const char* e = getenv("DPAC_PGX_W");  // read per launch
+  if (e && e[0] == '0') return false;
+  const int K = a.width[l], H = a.width[l + 1];
+  return l >= 1 && K > 32 && H > 32 && K <= 208 && H <= kPgwCW && K % 4 == 0 && H % 4 == 0 &&
+         a.ztot % 4 == 0 && a.zoff[l] % 4 == 0 && a.zoff[l + 1] % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(a.z) & 15) == 0;
+}
+
+template <int NTI>
+int pgw_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
+  using PL = PgwPlan<NTI>;
+  auto k = k_param_grads_x3w<NTI>;
+  if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, PL::kSmem))
+    return (int)e;
+  hipLaunchKernelGGL(k, dim3((unsigned)nch), dim3(kPgwThreads), PL::kSmem, s, a, l);
+  return (int)hipGetLastError();
+}
+
+// one layer of the split-fp16 kernel: wide hidden layers one 256-column group of 16 waves
+// (pgx_w_ok), other wide outputs 1 x 8 waves (one column tile each, 128-column groups; see
+// pgx_wide16), outputs of <= 32 columns 8 x 1 waves over the row tiles
 int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   const int K = a.width[l], H = a.width[l + 1];
   const int nti = (K + 15) / 16;
+  if (pgx_w_ok(a, l)) {
+    if (nti <= 4) return pgw_launch<4>(a, l, nch, s);
+    if (nti <= 8) return pgw_launch<8>(a, l, nch, s);
+    return pgw_launch<13>(a, l, nch, s);  // K <= 208 (13 tiles: 128 VGPRs without spills in the loop)
+  }
   if (H <= 32) {
     const int ntj = (H + 15) / 16, nt8 = (nti + 7) / 8;
     const dim3 grid((unsigned)nch, 1u);
@@ -242,7 +271,7 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
           if (hipError_t e = hipGetLastError()) return (int)e;
         }
         const int64_t n = a.ptot + a.width[a.L + 1];
-        hipLaunchKernelGGL(k_param_grads_reduce<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s0,
+        hipLaunchKernelGGL(k_param_grads_reduce<float>, dim3((unsigned)((n + kRedCols - 1) / kRedCols)), dim3(256), 0, s0,
                            a, (int)nch, (float)gamma_scale, (float*)out);
         return (int)hipGetLastError();
       }
@@ -274,7 +303,7 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
     if (hipError_t e = hipStreamWaitEvent(s0, fk->join, 0)) return (int)e;
   }
   const int64_t n = a.ptot + a.width[a.L + 1];
-  hipLaunchKernelGGL(k_param_grads_reduce<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s0,
+  hipLaunchKernelGGL(k_param_grads_reduce<T>, dim3((unsigned)((n + kRedCols - 1) / kRedCols)), dim3(256), 0, s0,
                      a, (int)nch, (T)gamma_scale, (T*)out);
   return (int)hipGetLastError();
 }

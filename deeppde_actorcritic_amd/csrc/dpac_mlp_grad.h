@@ -263,27 +263,42 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
   }
 }
 
-// out[p] = Σ_c part[c][p] in chunk order; gamma entries times rs; the bias
-// gradient db = s_{L+1} ⊙ dbeta_{L+1} appended at out[ptot ...].
+// out[p] = Σ_c part[c][p]; gamma entries times rs; the bias gradient db = s_{L+1} ⊙ dbeta_{L+1}
+// appended at out[ptot ...].  A workgroup owns kRedCols consecutive entries; its kRedSlices
+// wavefront halves each sum the chunks c ≡ slice (mod kRedSlices), 8 loads in flight, and the
+// slices are added in slice order through LDS (a fixed order: deterministic).  One thread per
+// entry summing all chunks in turn waited out nchunks / 8 load latencies (tens of µs at 256
+// chunks, the V network's reduce on the critic's critical path).
+constexpr int kRedCols = 32, kRedSlices = 8;  // 256 threads
 template <typename T>
 __global__ __launch_bounds__(256) void k_param_grads_reduce(const PgArgs<T> a, int nchunks,
                                                             T gamma_scale, T* out) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ T s_part[kRedSlices][kRedCols];
+  const int col = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
+  const int64_t p = (int64_t)blockIdx.x * kRedCols + col;
   const int L = a.L, Hout = a.width[L + 1];
-  if (p >= a.ptot + Hout) return;
+  const bool valid = p < a.ptot + Hout;
   const bool is_b = p >= a.ptot;
-  const int64_t src = is_b ? a.off_beta[L + 1] + (p - a.ptot) : p;
-  const T* col = a.part + src;
+  const int64_t src = !valid ? 0 : is_b ? a.off_beta[L + 1] + (p - a.ptot) : p;
+  const T* col_p = a.part + src;
   T s = 0;
-  int c = 0;
-  for (; c + 8 <= nchunks; c += 8) {  // 8 loads in flight, summed in chunk order
-    T v[8];
+  if (valid) {
+    int c = sl;
+    for (; c + 7 * kRedSlices < nchunks; c += 8 * kRedSlices) {  // 8 loads in flight
+      T v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = col[(int64_t)(c + u) * a.ptot];
+      for (int u = 0; u < 8; ++u) v[u] = col_p[(int64_t)(c + u * kRedSlices) * a.ptot];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; c < nchunks; c += kRedSlices) s += col_p[(int64_t)c * a.ptot];
   }
-  for (; c < nchunks; ++c) s += col[(int64_t)c * a.ptot];
+  s_part[sl][col] = s;
+  __syncthreads();
+  if (sl != 0 || !valid) return;
+  s = s_part[0][col];
+#pragma unroll
+  for (int k = 1; k < kRedSlices; ++k) s += s_part[k][col];
   if (is_b) {
     s = a.scale[L + 1][p - a.ptot] * s;
   } else if (p < a.off_beta[0]) {  // gamma block comes first

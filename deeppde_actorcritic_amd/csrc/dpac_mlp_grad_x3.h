@@ -48,6 +48,9 @@ constexpr int kPgxSR = 32;  // rows per sub-chunk = the MFMA's K
 #define DPAC_PGX_DEPTH 1  // register stages of loads in flight (2 measured: no gain, 0.628 vs 0.628 ms at 204 800 rows)
 #endif
 constexpr int kPgxDepth = DPAC_PGX_DEPTH;
+#ifndef DPAC_PGX_ROWDESC
+#define DPAC_PGX_ROWDESC 0  // timing knob: per-row buffer descriptors in the staging loads
+#endif
 static_assert(kPgxDepth == 1 || kPgxDepth == 2, "1 or 2 stages");
 constexpr float kPgxLo = 4096.f, kPgxLoInv = 1.f / 4096.f;
 
@@ -113,6 +116,9 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = wave / WJ, wj = wave % WJ;
   const int rb = tid / FL, fl = tid % FL;
+  static_assert(FL % 64 == 0, "a wave's lanes share one row block");
+  const int rbu = __builtin_amdgcn_readfirstlane(rb);
+  (void)rbu;
   const int64_t chunk = blockIdx.x;
   const int64_t r_begin = chunk * a.rows_per_chunk;
   const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
@@ -158,6 +164,33 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
 #pragma unroll
     for (int jj = 0; jj < NTJ; ++jj) acc[ti][jj] = pgf4{0.f, 0.f, 0.f, 0.f};
 
+#if DPAC_PGX_ROWDESC
+  // loads of the 32 rows at r0: one descriptor per row (wave-uniform: a wave's lanes share
+  // rb), based at the row and sized to it (0 past the chunk's end, so those rows read 0 and
+  // add nothing); the lane offsets are the column offsets alone, so no per-row VGPR offsets
+  // are hoisted out of the row loop (208 -> 180 VGPRs for the wide layers)
+  auto issue = [&](int64_t r0, PgxStage<QA, QB, L0>& st) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t row = r0 + 8 * rbu + i;
+      const bool in = row < r_end;
+      const auto rA = make_rsrc(srcA + row * ldA, in ? (uint32_t)K * 4u : 0u);
+      const auto rG = make_rsrc(gA + row * a.gtot, (in && L0) ? (uint32_t)K * 4u : 0u);
+      const auto rB = make_rsrc(gB + row * a.gtot, in ? (uint32_t)(H - col0) * 4u : 0u);
+      const auto rZ = make_rsrc(zB + row * a.ztot, in ? (uint32_t)(H - col0) * 4u : 0u);
+#pragma unroll
+      for (int q = 0; q < QA; ++q) {
+        st.a[q][i] = buf_load_elem<float>(rA, offA[q]);
+        if constexpr (L0) st.g0[q][i] = first ? buf_load_elem<float>(rG, offG0[q]) : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        st.gb[q][i] = buf_load_elem<float>(rB, offB[q]);
+        st.zb[q][i] = buf_load_elem<float>(rZ, offB[q]);
+      }
+    }
+  };
+#else
   // loads of the 32 rows at r0: descriptors based at row r0 ending at the chunk's last row
   // (rows past it read 0, so their G is 0 and they add nothing); masked columns carry kOOB
   auto issue = [&](int64_t r0, PgxStage<QA, QB, L0>& st) {
@@ -181,6 +214,7 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
       }
     }
   };
+#endif
 
   const int fq = lane >> 4, fi = lane & 15;  // fragment: row block, feature / column in the tile
   // one sub-chunk of 32 rows from its staged registers `st`, which are then refilled with
@@ -362,6 +396,236 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
     }
     part[a.off_beta[0] + tid] = sb;
     part[a.off_gamma[0] + tid] = ss;
+  }
+  if (bad) x3_flag(a.status);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// k_param_grads_x3w: the wide hidden layers (K and H in (32, 256], l >= 1) with ONE 256-column
+// group per chunk, so the A operand (z_l) is read once per chunk instead of once per 128-column
+// group (round 4; the two-group kernel read 0.78 GB per 204 800-row layer for 0.49 GB of A, G
+// and z).  The same sums, splits, column scaling and partial layout as k_param_grads_x3.
+//
+// 16 wavefronts (1 024 threads, one column tile each).  A 1 024-thread workgroup has 128 VGPRs
+// per lane, too few to hold the 13 accumulator tiles AND a register stage of A, G and z (the
+// register-staged 16-wave build spilled).  So z_l (A) and z_{l+1} (for the BN scale sums) reach
+// LDS by LDS-DMA (global_load_lds_dwordx4, one instruction per row and wavefront: 32 rows over
+// 16 wavefronts), and only G_{l+1} goes through registers (8 per lane).  Rows past the chunk's
+// end DMA the chunk's last row again (finite values; their G loads read 0, so they add nothing).
+// LDS: images A [2][4][KP][8] + B [3][4][256][8] halves, raw A and raw z [32][256] floats, the
+// column maxima / factors / exponents: 145 KB at KP = 208.
+// Requires 16-byte aligned rows: ztot, zoff[l], zoff[l+1] multiples of 4 (launch() checks).
+constexpr int kPgwThreads = 1024;
+constexpr int kPgwCW = 256;
+template <int NTI>
+struct PgwPlan {
+  static constexpr int KP = 16 * NTI;
+  static constexpr int kImgA = 2 * 4 * KP * 8 * 2;           // bytes
+  static constexpr int kImgB = 3 * 4 * kPgwCW * 8 * 2;
+  static constexpr int kRaw = kPgxSR * kPgwCW * 4;            // one raw [32][256] float block
+  static constexpr int kRawA = kImgA + kImgB;
+  static constexpr int kRawZ = kRawA + kRaw;
+  static constexpr int kCol = kRawZ + kRaw;                   // s_cmax [4][256], s_cfac, s_cexp
+  static constexpr int kSmem = kCol + (4 * kPgwCW + 2 * kPgwCW) * 4;
+  static_assert(4 * 2 * kPgwCW * 4 <= kRawA, "BN sums' reduction fits the image bytes");
+};
+
+// One wavefront copies one row (bytes <= 1 024, a multiple of 16) from global src to LDS dst
+// with global_load_lds_dwordx4: lane l moves bytes [16 l, 16 l + 16); lanes past the end read
+// the row's first 16 bytes again (in bounds) into their own slot of the 1 KB destination.
+// Inline asm (M0 holds the LDS base): the compiler cannot see the LDS write, so the caller
+// waits with s_waitcnt vmcnt(0) before the barrier that publishes the row.
+// The row address is wave-uniform (an SGPR pair, the saddr form); the lane's 32-bit offset
+// `voff` (16 l, or 0 past the row's end) is the only VGPR operand.
+__device__ __forceinline__ uint32_t pgw_lane_off(uint32_t bytes, int lane) {
+  const uint32_t off = (uint32_t)lane * 16u;
+  return off < bytes ? off : 0u;
+}
+__device__ __forceinline__ void pgw_row_dma(const float* src, uint32_t voff, unsigned char* dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)dst);
+  // readfirstlane returns int: widen through uint32_t (a sign-extended low word would set the
+  // high 32 bits of the address)
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)src);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)src >> 32));
+  const uint64_t base = lo | (hi << 32);
+  int keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(m0), "s"(base) : "memory");
+}
+
+template <int NTI>
+__global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<float> a, const int l) {
+  using PL = PgwPlan<NTI>;
+  constexpr int KP = PL::KP, CW = kPgwCW;
+  static_assert(KP <= 256, "one staging thread per feature");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // PL::kSmem bytes (dynamic)
+  _Float16* const sA = reinterpret_cast<_Float16*>(smem);
+  _Float16* const sB = reinterpret_cast<_Float16*>(smem + PL::kImgA);
+  const float* const rawA = reinterpret_cast<const float*>(smem + PL::kRawA);
+  const float* const rawZ = reinterpret_cast<const float*>(smem + PL::kRawZ);
+  float* const s_cmax = reinterpret_cast<float*>(smem + PL::kCol);
+  float* const s_cfac = s_cmax + 4 * CW;
+  int* const s_cexp = reinterpret_cast<int*>(s_cfac + CW);
+  if (x3_status_set(a.status)) return;  // fell back: the f32 kernel after this one does the work
+  bool bad = false;
+  const int K = a.width[l], H = a.width[l + 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = the column tile
+  const int rb = tid >> 8, fl = tid & 255;                     // staging: 8-row block, feature / column
+  const int rbu = __builtin_amdgcn_readfirstlane(rb);
+  const int64_t chunk = blockIdx.x;
+  const int64_t r_begin = chunk * a.rows_per_chunk;
+  const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
+  const bool last = l == a.L;
+  const float* srcA = a.z + a.zoff[l];
+  const float* gB = a.G + a.goff[l + 1];
+  const float* zB = a.z + a.zoff[l + 1];
+  const int64_t ld = a.ztot;
+  const bool fa = fl < K, fb = fl < H;
+  const float sa = fa ? a.scale[l][fl] : 0.f, ha = fa ? a.shift[l][fl] : 0.f;
+  const float sbv = fb ? a.scale[l + 1][fl] : 0.f, bbv = (fb && last) ? a.bias[fl] : 0.f;
+  const uint32_t offB = fb ? (uint32_t)fl * 4u : kOOB;
+  float csb_b = 0.f, csb_s = 0.f;
+  int cexp = -100;
+  pgf4 acc[NTI];  // 2^12 x (the column-scaled) dW tile: features 16 ti + 4 fq .., column 16 wave + fi
+#pragma unroll
+  for (int ti = 0; ti < NTI; ++ti) acc[ti] = pgf4{0.f, 0.f, 0.f, 0.f};
+  float gst[8];  // G_{l+1} at rows 8 rb + i, column fl (the register stage)
+  const uint32_t voffA = pgw_lane_off((uint32_t)K * 4u, lane), voffZ = pgw_lane_off((uint32_t)H * 4u, lane);
+
+  // the 32 rows at r0: z_l and z_{l+1} rows by LDS-DMA (wavefront w: rows 2w, 2w + 1),
+  // G_{l+1} through registers with one descriptor per row (wave-uniform rb)
+  auto issue = [&](int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = 2 * wave + j;
+      const int64_t row = min(r0 + i, r_end - 1);
+      pgw_row_dma(srcA + row * ld, voffA, smem + PL::kRawA + i * CW * 4);
+      pgw_row_dma(zB + row * ld, voffZ, smem + PL::kRawZ + i * CW * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t row = r0 + 8 * rbu + i;
+      const auto rB = make_rsrc(gB + row * a.gtot, row < r_end ? (uint32_t)H * 4u : 0u);
+      gst[i] = buf_load_elem<float>(rB, offB);
+    }
+  };
+
+  const int fq = lane >> 4, fi = lane & 15;
+  const _Float16* const aBase = sA + (fq * KP + fi) * 8;  // + (part 4 KP + 16 ti) 8: immediates
+  const int cT = wave * 16 + fi;                           // this lane's column in the group
+  const _Float16* const bBase = sB + (fq * CW + cT) * 8;
+  issue(r_begin);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += kPgxSR) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wavefront's row DMA (and G loads)
+    __syncthreads();  // raw rows in LDS; the previous sub-chunk's fragment reads are done
+    {  // A: feature fl of rows 8 rb .. + 7, the forward's BN and activation, split
+      if (fl < KP) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float y = ha + rawA[(8 * rb + i) * CW + fl] * sa;
+          v[i] = fa ? y + fmaxf(y, 0.f) : 0.f;  // l >= 1: hidden activations
+        }
+        pgh8 h, lo;
+        pgx_split8(v, h, lo);
+        bad |= x3_bad4(v[0], v[1], v[2], v[3]) | x3_bad4(v[4], v[5], v[6], v[7]);
+        *reinterpret_cast<pgh8*>(sA + ((0 * 4 + rb) * KP + fl) * 8) = h;
+        *reinterpret_cast<pgh8*>(sA + ((1 * 4 + rb) * KP + fl) * 8) = lo;
+      }
+    }
+    float vb[8];
+    {  // B: column fl, its sums and the sub-chunk's column max
+      float m = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float gv = gst[i];
+        vb[i] = gv * sbv;
+        m = fmaxf(m, fabsf(vb[i]));
+        csb_b += gv;
+        csb_s += gv * (rawZ[(8 * rb + i) * CW + fl] + bbv);  // bbv = 0 unless the output layer
+      }
+      s_cmax[rb * CW + fl] = m;
+    }
+    __syncthreads();  // the column maxima; every raw row read
+    {
+      const float m = fmaxf(fmaxf(s_cmax[fl], s_cmax[CW + fl]), fmaxf(s_cmax[2 * CW + fl], s_cmax[3 * CW + fl]));
+      int e = cexp;
+      if (m > 0.f && m < 3.0e38f) {
+        int em = 0;
+        (void)frexpf(m, &em);
+        e = em > cexp ? em : cexp;
+      }
+      const float sc = ldexpf(1.f, 3 - e);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vb[i] *= sc;
+      pgh8 h, lo, h12;
+      pgx_split8(vb, h, lo);
+      bad |= x3_bad4(vb[0], vb[1], vb[2], vb[3]) | x3_bad4(vb[4], vb[5], vb[6], vb[7]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) h12[i] = h[i] * (_Float16)kPgxLo;  // exact: |h| < 8
+      *reinterpret_cast<pgh8*>(sB + ((0 * 4 + rb) * CW + fl) * 8) = h;
+      *reinterpret_cast<pgh8*>(sB + ((1 * 4 + rb) * CW + fl) * 8) = lo;
+      *reinterpret_cast<pgh8*>(sB + ((2 * 4 + rb) * CW + fl) * 8) = h12;
+      if (rb == 0) {
+        s_cfac[fl] = ldexpf(1.f, cexp - e);
+        s_cexp[fl] = e;
+      }
+      cexp = e;
+    }
+    // the next sub-chunk's rows (the raw rows are read; vb no longer needs gst): they land
+    // during this sub-chunk's MFMAs
+    if (r0 + kPgxSR < r_end) issue(r0 + kPgxSR);
+    __syncthreads();  // the images
+    const pgh8 bh = *reinterpret_cast<const pgh8*>(bBase);
+    const pgh8 bl = *reinterpret_cast<const pgh8*>(bBase + 4 * CW * 8);
+    const pgh8 b12 = *reinterpret_cast<const pgh8*>(bBase + 2 * 4 * CW * 8);
+    const float f = s_cfac[cT];
+    if (__any(f != 1.f)) {
+#pragma unroll
+      for (int ti = 0; ti < NTI; ++ti) acc[ti] *= f;
+    }
+#pragma unroll
+    for (int ti = 0; ti < NTI; ++ti) {
+      const pgh8 xh = *reinterpret_cast<const pgh8*>(aBase + 16 * ti * 8);
+      const pgh8 xl = *reinterpret_cast<const pgh8*>(aBase + (4 * KP + 16 * ti) * 8);
+      acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, b12, acc[ti], 0, 0, 0);
+      acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, bl, acc[ti], 0, 0, 0);
+      acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, bh, acc[ti], 0, 0, 0);
+    }
+  }
+
+  // ---- this chunk's partial dW_l: lane holds features 16 ti + 4 fq .. +3, column cT ----
+  float* part = a.part + chunk * a.ptot;
+  {
+    const float us = ldexpf(1.f, s_cexp[cT] - 3 - 12);  // undo 2^12 and the column scale
+#pragma unroll
+    for (int ti = 0; ti < NTI; ++ti) {
+      const pgf4 c = acc[ti] * us;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int k = 16 * ti + 4 * fq + v;
+        if (k < K && cT < H) part[a.off_W[l] + (int64_t)k * H + cT] = c[v];
+      }
+    }
+  }
+  // ---- BN column sums: combine the 4 row blocks through LDS (reusing the images) ----
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  red[(rb * 2 + 0) * CW + fl] = csb_b;
+  red[(rb * 2 + 1) * CW + fl] = csb_s;
+  __syncthreads();
+  if (tid < CW && tid < H) {
+    float sb = 0.f, ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sb += red[(w * 2 + 0) * CW + tid];
+      ss += red[(w * 2 + 1) * CW + tid];
+    }
+    part[a.off_beta[l + 1] + tid] = sb;
+    part[a.off_gamma[l + 1] + tid] = ss;
   }
   if (bad) x3_flag(a.status);
 }

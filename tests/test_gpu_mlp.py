@@ -89,6 +89,7 @@ def test_param_grads_vs_torch(widths, R, dtype):
     ((5, 256, 256, 256, 256, 1), 3001),    # 16-tile inputs: those layers take the f32 kernel
     ((4, 7, 2), 1),                        # one row; the input layer into 7 takes the f32 kernel
     ((10, 48, 130, 33, 10), 4099),         # widths that split MFMA tiles and column groups
+    ((12, 52, 100, 36, 8), 1234),          # merged-group kernel at other widths (k_param_grads_x3w)
     ((20, 200, 200, 200, 20), 204800)])    # the lqr_d20 critic G network's N*B rows
 @pytest.mark.parametrize("gscale", [1.0, 1e-6, "ramp"])
 def test_param_grads_split_fp16_vs_torch(widths, R, gscale, monkeypatch):
@@ -129,6 +130,37 @@ def test_param_grads_split_fp16_vs_torch(widths, R, gscale, monkeypatch):
         worst = max(worst, err)
         assert err <= 2e-5 and err <= 4 * err32 + 5e-6, (a.shape, err, err32)
     print(f"\n[x3 param grads {widths} R={R} G~{gscale}] max rel err {worst:.2e}")
+
+
+@pytest.mark.parametrize("widths,R", [
+    ((20, 200, 200, 200, 20), 20000),      # the lqr_d20 networks
+    ((20, 200, 200, 200, 20), 777),        # ragged: the last chunk ends inside a sub-chunk
+    ((12, 52, 100, 36, 8), 1234)])         # 4- and 7-tile inputs, 100- and 36-column outputs
+@pytest.mark.parametrize("gscale", [1.0, "ramp"])
+def test_param_grads_merged_group_kernel_bitwise(widths, R, gscale, monkeypatch):
+    """The wide hidden layers' merged-group split-fp16 kernel (k_param_grads_x3w: one
+    256-column group, z rows by LDS-DMA) forms the same products in the same order as the
+    two-group kernel (DPAC_PGX_W=0): the gradients are bitwise equal, column rescaling
+    included (ramp)."""
+    scales, shifts, Ws, b = random_net(widths, torch.float32, seed=3 * R + len(widths))
+    g = torch.Generator().manual_seed(R + 1)
+    rnd = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(torch.float32).to(DEV)
+    x, z, G = rnd(R, widths[0]), rnd(R, sum(widths[1:])), rnd(R, sum(widths))
+    if gscale == "ramp":
+        G = G * torch.logspace(-9, 0, R, dtype=torch.float64).to(torch.float32).to(DEV).unsqueeze(1)
+    view = ops.MlpView(scales, shifts, Ws, b, False, weights_x3=[_x3_image(W) for W in Ws])
+    like = scales + shifts + Ws + [b]
+    monkeypatch.delenv("DPAC_PG_X3", raising=False)
+    monkeypatch.delenv("DPAC_PGX_W", raising=False)
+    merged = ops.mlp_param_grads(view, x, z, G, like)
+    monkeypatch.setenv("DPAC_PGX_W", "0")
+    two = ops.mlp_param_grads(view, x, z, G, like)
+    monkeypatch.setenv("DPAC_PG_X3", "0")
+    f32 = ops.mlp_param_grads(view, x, z, G, like)
+    assert any(not torch.equal(a, c) for a, c in zip(merged, f32)), "the split-fp16 kernels did not run"
+    for a, c in zip(merged, two):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, c), float((a - c).abs().max())
 
 
 def test_param_grads_strided_input_and_bad_args():

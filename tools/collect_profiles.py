@@ -48,6 +48,11 @@ def main(tag):
         txt = open(hl).read()
         if txt.lstrip().startswith("{"):
             open(os.path.join(PROF, f"{tag}_rocprof_headline.json"), "w").write(txt)
+    hm = os.path.join(OUT, "headline_mall.log")  # the same over the --mall run
+    if os.path.exists(hm):
+        txt = open(hm).read()
+        if txt.lstrip().startswith("{"):
+            open(os.path.join(PROF, f"{tag}_rocprof_headline_mall.json"), "w").write(txt)
     pm = os.path.join(OUT, "pmc_mlp", "summary.json")  # tools/pmc_mlp.sh
     if os.path.exists(pm):
         shutil.copy(pm, os.path.join(PROF, f"{tag}_pmc_mlp.json"))

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Time the row-parallel MLP kernels at the critic G network's shape (R = N*B rows) with
 split-fp16 MFMA (DPAC_MLP_MATH=x3) and exact f32 MFMA: forward with saves, the fused-TD1
-forward, and the backward chain (dpac_mlp_rows_bwd)."""
+forward, and the backward chain (dpac_mlp_rows_bwd); with --pg also the parameter gradients.
+
+    python tools/probe_x3.py [R] [f32,x3] [--pg]"""
 import json
 import os
 import sys
@@ -25,7 +27,8 @@ def timeit(fn, reps=20):
 
 
 def main():
-    R = int(sys.argv[1]) if len(sys.argv) > 1 else 204800
+    argv = [a for a in sys.argv if not a.startswith("--")]
+    R = int(argv[1]) if len(argv) > 1 else 204800
     from deeppde_actorcritic_amd import ops, _lib
     from deeppde_actorcritic_amd import solver as psol
     from deeppde_actorcritic_amd import equation as peq
@@ -41,7 +44,7 @@ def main():
     g = torch.randn(R, 20, device="cuda") * 1e-3
     flop = 2 * R * (20 * 200 + 2 * 200 * 200 + 200 * 20)
     params = [p.detach() for p in net.trainable_variables()]
-    maths = sys.argv[2].split(",") if len(sys.argv) > 2 else ["f32", "x3"]
+    maths = argv[2].split(",") if len(argv) > 2 else ["f32", "x3"]
     for math in maths:
         ops.MLP_MATH = math
         view = net.mlp_view()
@@ -57,6 +60,9 @@ def main():
         res = {"fwd_saves": timeit(lambda: ops.mlp_rows(view, x, save=True)),
                "fwd_td1_saves": timeit(lambda: ops.mlp_rows_td1(eqp, view, x, u, dw, save=True)),
                "bwd_chain": timeit(bwd)}
+        if "--pg" in sys.argv:  # the parameter gradients (every layer + the chunk reduce)
+            bwd()
+            res["param_grads"] = timeit(lambda: ops.mlp_param_grads(view, x, z, G, params))
         for k, ms in res.items():
             print(json.dumps({"math": math, "R": R, "what": k, "us": ms * 1e3,
                               "TFLOPs_f32_equiv": flop / ms / 1e9}), flush=True)

@@ -9,7 +9,7 @@ source tools/gpu_steps.sh
 export TMPDIR=/tmp
 R=$PWD
 rm -f gpurun_out/steps.log
-rm -rf gpurun_out/prof_kt gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof_train
+rm -rf gpurun_out/prof_kt gpurun_out/prof_mall gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof_train
 if [ -z "${SKIP_TESTS:-}" ]; then
   run 900 pytest_gpu python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread
   run 300 smoke python -u -c "import __graft_entry__ as g; g.smoke()"
@@ -19,6 +19,9 @@ run 400 bench python -u bench.py --steps 200 --warmup 20
 # the mean over exactly the W + K headline launches: the MALL variant runs only with --mall)
 run 400 prof_kt rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5
 run 60 headline python tools/rocprof_headline.py gpurun_out/prof_kt/run_kernel_trace.csv gpurun_out/prof_kt.log --steps 20 --warmup 5 --stats gpurun_out/prof_kt/run_kernel_stats.csv
+# the MALL-resident (one buffer set) variant on its own, for the cold / resident comparison
+run 300 prof_mall rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_mall -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --mall --no-cpu-baseline --no-train
+run 60 headline_mall python tools/rocprof_headline.py gpurun_out/prof_mall/run_kernel_trace.csv gpurun_out/prof_mall.log --steps 20 --warmup 5 --mall
 run 300 prof_train rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_train -o run --output-format csv -- python tools/train_bench.py --iters 3 --warmup 1 --dtype float32
 run 300 pmc_fetch rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
 run 300 pmc_write rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
