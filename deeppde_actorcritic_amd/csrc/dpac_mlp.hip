@@ -175,22 +175,27 @@ inline bool pgx_wide16() {
   return e && e[0] == '1' && e[1] == '6';
 }
 
-// The merged-group kernel for a wide hidden layer (k_param_grads_x3w: A read once per chunk):
-// rows of z_l and z_{l+1} move by 16-byte LDS-DMA, so every row start must be 16-byte aligned.
-// DPAC_PGX_W=0 selects the two-group kernel (timing comparisons, tests).
+// The merged-group kernel (k_param_grads_x3w: one 256-column group, A read once per chunk) for
+// the wide hidden layers and for the input layer into a wide layer: rows of A, z_{l+1} (and G_0
+// for the input layer) move by 16-byte LDS-DMA, so every row start must be 16-byte aligned.
+// Outputs of <= 32 columns keep the 8-wavefront kernel (the merged-group one measured 78.5 vs
+// 75 us on the lqr_d20 output layer).  DPAC_PGX_W=0 selects the two-group kernels.
 inline bool pgx_w_ok(const PgArgs<float>& a, int l) {
   const char* e = getenv("DPAC_PGX_W");  // read per launch
   if (e && e[0] == '0') return false;
   const int K = a.width[l], H = a.width[l + 1];
-  return l >= 1 && K > 32 && H > 32 && K <= 208 && H <= kPgwCW && K % 4 == 0 && H % 4 == 0 &&
-         a.ztot % 4 == 0 && a.zoff[l] % 4 == 0 && a.zoff[l + 1] % 4 == 0 &&
-         (reinterpret_cast<uintptr_t>(a.z) & 15) == 0;
+  const bool out = H <= kPgwCW && H % 4 == 0 && a.ztot % 4 == 0 && a.zoff[l + 1] % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.z) & 15) == 0;
+  if (l == 0)  // BN_0's sums read G_0 rows too
+    return K <= 32 && H > 32 && K % 4 == 0 && a.ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 &&
+           a.gtot % 4 == 0 && a.goff[0] % 4 == 0 && (reinterpret_cast<uintptr_t>(a.G) & 15) == 0 && out;
+  return K > 32 && H > 32 && K <= 208 && K % 4 == 0 && a.zoff[l] % 4 == 0 && out;
 }
 
-template <int NTI>
+template <int NTI, bool L0 = false>
 int pgw_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
-  using PL = PgwPlan<NTI>;
-  auto k = k_param_grads_x3w<NTI>;
+  using PL = PgwPlan<NTI, L0>;
+  auto k = k_param_grads_x3w<NTI, L0>;
   if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, PL::kSmem))
     return (int)e;
@@ -205,6 +210,7 @@ int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   const int K = a.width[l], H = a.width[l + 1];
   const int nti = (K + 15) / 16;
   if (pgx_w_ok(a, l)) {
+    if (l == 0) return nti <= 1 ? pgw_launch<1, true>(a, l, nch, s) : pgw_launch<2, true>(a, l, nch, s);
     if (nti <= 4) return pgw_launch<4>(a, l, nch, s);
     if (nti <= 8) return pgw_launch<8>(a, l, nch, s);
     return pgw_launch<13>(a, l, nch, s);  // K <= 208 (13 tiles: 128 VGPRs without spills in the loop)

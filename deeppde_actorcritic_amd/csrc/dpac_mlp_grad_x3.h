@@ -402,10 +402,12 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
 
 
 // ---------------------------------------------------------------------------------------------
-// k_param_grads_x3w: the wide hidden layers (K and H in (32, 256], l >= 1) with ONE 256-column
-// group per chunk, so the A operand (z_l) is read once per chunk instead of once per 128-column
-// group (round 4; the two-group kernel read 0.78 GB per 204 800-row layer for 0.49 GB of A, G
-// and z).  The same sums, splits, column scaling and partial layout as k_param_grads_x3.
+// k_param_grads_x3w: the wide hidden layers (K in (32, 208], H in (32, 256], l >= 1) and the
+// input layer into a wide layer (L0: K <= 32, A = the network input, plus BN_0's sums from G_0)
+// with ONE 256-column group per chunk, so the A operand is read once per chunk instead of once
+// per 128-column group (round 4; the two-group kernel read 0.78 GB per 204 800-row layer for
+// 0.49 GB of A, G and z).  The same sums, splits, column scaling and partial layout as
+// k_param_grads_x3, in the same order: bitwise its results.
 //
 // 16 wavefronts (1 024 threads, one column tile each).  A 1 024-thread workgroup has 128 VGPRs
 // per lane, too few to hold the 13 accumulator tiles AND a register stage of A, G and z (the
@@ -418,7 +420,7 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
 // Requires 16-byte aligned rows: ztot, zoff[l], zoff[l+1] multiples of 4 (launch() checks).
 constexpr int kPgwThreads = 1024;
 constexpr int kPgwCW = 256;
-template <int NTI>
+template <int NTI, bool L0 = false>
 struct PgwPlan {
   static constexpr int KP = 16 * NTI;
   static constexpr int kImgA = 2 * 4 * KP * 8 * 2;           // bytes
@@ -426,9 +428,11 @@ struct PgwPlan {
   static constexpr int kRaw = kPgxSR * kPgwCW * 4;            // one raw [32][256] float block
   static constexpr int kRawA = kImgA + kImgB;
   static constexpr int kRawZ = kRawA + kRaw;
-  static constexpr int kCol = kRawZ + kRaw;                   // s_cmax [4][256], s_cfac, s_cexp
+  static constexpr int kRawG0 = kRawZ + kRaw;                 // L0: G_0 rows (the BN_0 sums)
+  static constexpr int kCol = kRawG0 + (L0 ? kRaw : 0);       // s_cmax [4][256], s_cfac, s_cexp
   static constexpr int kSmem = kCol + (4 * kPgwCW + 2 * kPgwCW) * 4;
-  static_assert(4 * 2 * kPgwCW * 4 <= kRawA, "BN sums' reduction fits the image bytes");
+  static_assert(4 * 2 * kPgwCW * 4 + (L0 ? 4 * 2 * KP * 4 : 0) <= kRawA, "BN sums' reduction fits the image bytes");
+  static_assert(kSmem <= 160 * 1024, "LDS");
 };
 
 // One wavefront copies one row (bytes <= 1 024, a multiple of 16) from global src to LDS dst
@@ -455,9 +459,9 @@ __device__ __forceinline__ void pgw_row_dma(const float* src, uint32_t voff, uns
                : "=&s"(keep) : "v"(voff), "s"(m0), "s"(base) : "memory");
 }
 
-template <int NTI>
+template <int NTI, bool L0 = false>
 __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<float> a, const int l) {
-  using PL = PgwPlan<NTI>;
+  using PL = PgwPlan<NTI, L0>;
   constexpr int KP = PL::KP, CW = kPgwCW;
   static_assert(KP <= 256, "one staging thread per feature");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // PL::kSmem bytes (dynamic)
@@ -479,7 +483,8 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   const int64_t r_begin = chunk * a.rows_per_chunk;
   const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
   const bool last = l == a.L;
-  const float* srcA = a.z + a.zoff[l];
+  const float* srcA = L0 ? a.x : a.z + a.zoff[l];  // L0: the network input (l = 0)
+  const int64_t ldA = L0 ? a.ldx : a.ztot;
   const float* gB = a.G + a.goff[l + 1];
   const float* zB = a.z + a.zoff[l + 1];
   const int64_t ld = a.ztot;
@@ -488,10 +493,11 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   const float sbv = fb ? a.scale[l + 1][fl] : 0.f, bbv = (fb && last) ? a.bias[fl] : 0.f;
   const uint32_t offB = fb ? (uint32_t)fl * 4u : kOOB;
   float csb_b = 0.f, csb_s = 0.f;
+  float cs0_b = 0.f, cs0_s = 0.f;  // L0: BN_0's sums, feature fl (rows of this thread's block)
   int cexp = -100;
-  pgf4 acc[NTI];  // 2^12 x (the column-scaled) dW tile: features 16 ti + 4 fq .., column 16 wave + fi
+  pgf4 acc[NTI];  // 2^12 x (the column-scaled) dW tile: features 16 t + 4 fq .., column 16 wave + fi
 #pragma unroll
-  for (int ti = 0; ti < NTI; ++ti) acc[ti] = pgf4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NTI; ++t) acc[t] = pgf4{0.f, 0.f, 0.f, 0.f};
   float gst[8];  // G_{l+1} at rows 8 rb + i, column fl (the register stage)
   const uint32_t voffA = pgw_lane_off((uint32_t)K * 4u, lane), voffZ = pgw_lane_off((uint32_t)H * 4u, lane);
 
@@ -502,8 +508,9 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
     for (int j = 0; j < 2; ++j) {
       const int i = 2 * wave + j;
       const int64_t row = min(r0 + i, r_end - 1);
-      pgw_row_dma(srcA + row * ld, voffA, smem + PL::kRawA + i * CW * 4);
+      pgw_row_dma(srcA + row * ldA, voffA, smem + PL::kRawA + i * CW * 4);
       pgw_row_dma(zB + row * ld, voffZ, smem + PL::kRawZ + i * CW * 4);
+      if constexpr (L0) pgw_row_dma(a.G + a.goff[0] + row * a.gtot, voffA, smem + PL::kRawG0 + i * CW * 4);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -514,8 +521,8 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   };
 
   const int fq = lane >> 4, fi = lane & 15;
-  const _Float16* const aBase = sA + (fq * KP + fi) * 8;  // + (part 4 KP + 16 ti) 8: immediates
-  const int cT = wave * 16 + fi;                           // this lane's column in the group
+  const _Float16* const aBase = sA + (fq * KP + fi) * 8;  // + (part 4 KP + 16 t) 8: immediates
+  const int cT = wave * 16 + fi;                           // this lane's column in the group (past H: 0)
   const _Float16* const bBase = sB + (fq * CW + cT) * 8;
   issue(r_begin);
   for (int64_t r0 = r_begin; r0 < r_end; r0 += kPgxSR) {
@@ -526,8 +533,18 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
         float v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const float y = ha + rawA[(8 * rb + i) * CW + fl] * sa;
-          v[i] = fa ? y + fmaxf(y, 0.f) : 0.f;  // l >= 1: hidden activations
+          const float xv = rawA[(8 * rb + i) * CW + fl];
+          const float y = ha + xv * sa;
+          if constexpr (L0) {  // BN_0 only (solver.py:260-262); its sums over the chunk's rows
+            v[i] = fa ? y : 0.f;
+            if (fa && r0 + 8 * rb + i < r_end) {
+              const float g0 = reinterpret_cast<const float*>(smem + PL::kRawG0)[(8 * rb + i) * CW + fl];
+              cs0_b += g0;
+              cs0_s += g0 * xv;
+            }
+          } else {
+            v[i] = fa ? y + fmaxf(y, 0.f) : 0.f;  // l >= 1: hidden activations
+          }
         }
         pgh8 h, lo;
         pgx_split8(v, h, lo);
@@ -579,34 +596,36 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
     // during this sub-chunk's MFMAs
     if (r0 + kPgxSR < r_end) issue(r0 + kPgxSR);
     __syncthreads();  // the images
-    const pgh8 bh = *reinterpret_cast<const pgh8*>(bBase);
-    const pgh8 bl = *reinterpret_cast<const pgh8*>(bBase + 4 * CW * 8);
-    const pgh8 b12 = *reinterpret_cast<const pgh8*>(bBase + 2 * 4 * CW * 8);
-    const float f = s_cfac[cT];
-    if (__any(f != 1.f)) {
+    {
+      const pgh8 bh = *reinterpret_cast<const pgh8*>(bBase);
+      const pgh8 bl = *reinterpret_cast<const pgh8*>(bBase + 4 * CW * 8);
+      const pgh8 b12 = *reinterpret_cast<const pgh8*>(bBase + 2 * 4 * CW * 8);
+      const float f = s_cfac[cT];
+      if (__any(f != 1.f)) {
 #pragma unroll
-      for (int ti = 0; ti < NTI; ++ti) acc[ti] *= f;
-    }
+        for (int t = 0; t < NTI; ++t) acc[t] *= f;
+      }
 #pragma unroll
-    for (int ti = 0; ti < NTI; ++ti) {
-      const pgh8 xh = *reinterpret_cast<const pgh8*>(aBase + 16 * ti * 8);
-      const pgh8 xl = *reinterpret_cast<const pgh8*>(aBase + (4 * KP + 16 * ti) * 8);
-      acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, b12, acc[ti], 0, 0, 0);
-      acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, bl, acc[ti], 0, 0, 0);
-      acc[ti] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, bh, acc[ti], 0, 0, 0);
+      for (int t = 0; t < NTI; ++t) {
+        const pgh8 xh = *reinterpret_cast<const pgh8*>(aBase + 16 * t * 8);
+        const pgh8 xl = *reinterpret_cast<const pgh8*>(aBase + (4 * KP + 16 * t) * 8);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, b12, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, bl, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, bh, acc[t], 0, 0, 0);
+      }
     }
   }
 
-  // ---- this chunk's partial dW_l: lane holds features 16 ti + 4 fq .. +3, column cT ----
+  // ---- this chunk's partial dW_l: lane holds features 16 t + 4 fq .. +3, column cT ----
   float* part = a.part + chunk * a.ptot;
   {
     const float us = ldexpf(1.f, s_cexp[cT] - 3 - 12);  // undo 2^12 and the column scale
 #pragma unroll
-    for (int ti = 0; ti < NTI; ++ti) {
-      const pgf4 c = acc[ti] * us;
+    for (int t = 0; t < NTI; ++t) {
+      const pgf4 c = acc[t] * us;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const int k = 16 * ti + 4 * fq + v;
+        const int k = 16 * t + 4 * fq + v;
         if (k < K && cT < H) part[a.off_W[l] + (int64_t)k * H + cT] = c[v];
       }
     }
@@ -616,7 +635,22 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   float* red = reinterpret_cast<float*>(smem);
   red[(rb * 2 + 0) * CW + fl] = csb_b;
   red[(rb * 2 + 1) * CW + fl] = csb_s;
+  float* red0 = red + 4 * 2 * CW;  // L0: [4 rb][2][KP]
+  if (L0 && fl < KP) {
+    red0[(rb * 2 + 0) * KP + fl] = cs0_b;
+    red0[(rb * 2 + 1) * KP + fl] = cs0_s;
+  }
   __syncthreads();
+  if (L0 && tid < K) {
+    float sb = 0.f, ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sb += red0[(w * 2 + 0) * KP + tid];
+      ss += red0[(w * 2 + 1) * KP + tid];
+    }
+    part[a.off_beta[0] + tid] = sb;
+    part[a.off_gamma[0] + tid] = ss;
+  }
   if (tid < CW && tid < H) {
     float sb = 0.f, ss = 0.f;
 #pragma unroll

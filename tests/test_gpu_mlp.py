@@ -135,13 +135,15 @@ def test_param_grads_split_fp16_vs_torch(widths, R, gscale, monkeypatch):
 @pytest.mark.parametrize("widths,R", [
     ((20, 200, 200, 200, 20), 20000),      # the lqr_d20 networks
     ((20, 200, 200, 200, 20), 777),        # ragged: the last chunk ends inside a sub-chunk
-    ((12, 52, 100, 36, 8), 1234)])         # 4- and 7-tile inputs, 100- and 36-column outputs
+    ((12, 52, 100, 36, 8), 1234),          # 4- and 7-tile inputs, 100- and 36-column outputs
+    ((8, 64, 40, 12), 999)])               # a one-tile input layer, a 12-column output layer
 @pytest.mark.parametrize("gscale", [1.0, "ramp"])
 def test_param_grads_merged_group_kernel_bitwise(widths, R, gscale, monkeypatch):
-    """The wide hidden layers' merged-group split-fp16 kernel (k_param_grads_x3w: one
-    256-column group, z rows by LDS-DMA) forms the same products in the same order as the
-    two-group kernel (DPAC_PGX_W=0): the gradients are bitwise equal, column rescaling
-    included (ramp)."""
+    """The merged-group split-fp16 kernel (k_param_grads_x3w: one 256-column group, operand
+    rows by LDS-DMA; for the input layer, the hidden layers with more than 32 inputs and the
+    narrow output layer) forms the same products in the same order as the earlier kernels
+    (DPAC_PGX_W=0: two 128-column groups, or 8 waves over the row tiles for <= 32 columns): the
+    gradients, BN_0's sums included, are bitwise equal, column rescaling included (ramp)."""
     scales, shifts, Ws, b = random_net(widths, torch.float32, seed=3 * R + len(widths))
     g = torch.Generator().manual_seed(R + 1)
     rnd = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(torch.float32).to(DEV)
