@@ -53,6 +53,11 @@ def main(tag):
         txt = open(hm).read()
         if txt.lstrip().startswith("{"):
             open(os.path.join(PROF, f"{tag}_rocprof_headline_mall.json"), "w").write(txt)
+    pi = os.path.join(OUT, "pmc_iteration.log")  # tools/pmc_iteration.py over one training iteration
+    if os.path.exists(pi):
+        txt = open(pi).read()
+        if txt.lstrip().startswith("{"):
+            open(os.path.join(PROF, f"{tag}_pmc_iteration.json"), "w").write(txt)
     pm = os.path.join(OUT, "pmc_mlp", "summary.json")  # tools/pmc_mlp.sh
     if os.path.exists(pm):
         shutil.copy(pm, os.path.join(PROF, f"{tag}_pmc_mlp.json"))

@@ -20,5 +20,5 @@ for set in "${sets[@]}"; do
     python tools/probe_x3.py 204800 x3 > gpurun_out/pmc_mlp/pmc_rows_$i.log 2>&1 || exit 1
 done
 python tools/pmc_summary.py gpurun_out/pmc_mlp gpurun_out/pmc_mlp/summary.json \
-  --kernels "k_rollout_nn_x3<,k_rollout_nn_bwd_x3<,k_param_grads_x3<13,k_mlp_rows_fwd_x3,k_mlp_rows_bwd_x3" \
+  --kernels "k_rollout_nn_x3<,k_rollout_nn_bwd_x3<,k_param_grads_x3w<13,k_param_grads_x3w<2,k_mlp_rows_fwd_x3,k_mlp_rows_bwd_x3" \
   --note "lqr_d20 fp32 split-fp16 kernels: actor B=2048 N=100 (probe_bptt), critic rows 204800 (probe_x3)"

@@ -9,7 +9,7 @@ source tools/gpu_steps.sh
 export TMPDIR=/tmp
 R=$PWD
 rm -f gpurun_out/steps.log
-rm -rf gpurun_out/prof_kt gpurun_out/prof_mall gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof_train
+rm -rf gpurun_out/prof_kt gpurun_out/prof_mall gpurun_out/pmc_it_fetch gpurun_out/pmc_it_write gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof_train
 if [ -z "${SKIP_TESTS:-}" ]; then
   run 900 pytest_gpu python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread
   run 300 smoke python -u -c "import __graft_entry__ as g; g.smoke()"
@@ -26,3 +26,7 @@ run 300 prof_train rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_train 
 run 300 pmc_fetch rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
 run 300 pmc_write rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-variants
 run 900 pmc_mlp bash tools/pmc_mlp.sh
+# HBM bytes of one lqr_d20 training iteration (FETCH_SIZE and WRITE_SIZE in separate passes)
+run 300 pmc_it_fetch rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_it_fetch -o run --output-format csv -- python tools/train_bench.py --iters 3 --warmup 1 --dtype float32
+run 300 pmc_it_write rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_it_write -o run --output-format csv -- python tools/train_bench.py --iters 3 --warmup 1 --dtype float32
+run 60 pmc_iteration python tools/pmc_iteration.py gpurun_out/pmc_it_fetch/run_counter_collection.csv gpurun_out/pmc_it_write/run_counter_collection.csv
