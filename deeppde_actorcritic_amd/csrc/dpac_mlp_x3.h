@@ -61,12 +61,6 @@ static_assert(kX3MaxNT == 2, "the dispatch below covers 1..2 feature tiles per w
 
 __host__ __device__ constexpr int x3_chunks(int k) { return (k + 31) / 32; }
 
-#ifndef DPAC_X3_ADJ
-#define DPAC_X3_ADJ 0  // timing knob: a wave's two feature tiles adjacent (2w, 2w + 1) instead of (w, w + 8)
-#endif
-// the j-th feature tile of wave `wave`
-__device__ __forceinline__ int x3_tile(int wave, int j) { return DPAC_X3_ADJ ? 2 * wave + j : wave + kX3Waves * j; }
-
 // Timing-only builds (-DDPAC_X3_TRACE=1): lane 0 of every wavefront of the first 256
 // workgroups records the shader clock at fixed points (start, prologue done, then per layer
 // K loop done / layer barrier passed) into g_x3_trace, read by dpac_debug_x3_trace.
@@ -167,7 +161,7 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
   x3f4 ah[kX3RT][NT], al[kX3RT][NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    const int tile = x3_tile(wave, j);
+    const int tile = wave + kX3Waves * j;
     voff[j] = tile < ntiles ? (uint32_t)(tile * nch * 2048 + 16 * lane) : kOOB;
 #pragma unroll
     for (int rt = 0; rt < kX3RT; ++rt) ah[rt][j] = al[rt][j] = x3f4{0, 0, 0, 0};
@@ -263,8 +257,7 @@ template <class EPI>
 __device__ __forceinline__ bool x3_layer(const _Float16* in, int K, int Nout, const _Float16* Wx3, int wave,
                                          int lane, EPI& epi) {
   const int ntiles = (Nout + 15) / 16;
-  const int mine = DPAC_X3_ADJ ? (ntiles > 2 * wave ? (ntiles - 2 * wave < 2 ? ntiles - 2 * wave : 2) : 0)
-                               : (ntiles > wave ? (ntiles - wave + kX3Waves - 1) / kX3Waves : 0);
+  const int mine = ntiles > wave ? (ntiles - wave + kX3Waves - 1) / kX3Waves : 0;
   const int nch = x3_chunks(K);
   // straight-line layers for the shipped shapes (d <= 32: one chunk; 193..224 wide: seven)
   if (nch == 1) {
@@ -309,7 +302,7 @@ struct X3Args {
 };
 
 // the lane's feature quad f0 = 16 tile + 4 (l >> 4) and how many of its features exist
-__device__ __forceinline__ int x3_f0(int wave, int j, int lane) { return x3_tile(wave, j) * 16 + 4 * (lane >> 4); }
+__device__ __forceinline__ int x3_f0(int wave, int j, int lane) { return (wave + kX3Waves * j) * 16 + 4 * (lane >> 4); }
 __device__ __forceinline__ int x3_nvalid(int f0, int Nout) { return Nout - f0 < 0 ? 0 : (Nout - f0 > 4 ? 4 : Nout - f0); }
 
 // Forward epilogue of dense layer l: z -> save -> BN(z (+ b)) -> then by MODE: [y + relu(y)]
