@@ -167,13 +167,6 @@ int pgx_launch(const PgArgs<float>& a, int l, dim3 grid, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// Wide hidden layers (K and H both > 32): two 128-column groups of 8 wavefronts, each staging
-// A (default), or with DPAC_PGX_NW=16 one 256-column group of 16 wavefronts staging A once per
-// chunk (round 4 experiment: at 13 input tiles its 128-register budget spills 87 registers).
-inline bool pgx_wide16() {
-  const char* e = getenv("DPAC_PGX_NW");  // read per launch
-  return e && e[0] == '1' && e[1] == '6';
-}
 
 // The merged-group kernel (k_param_grads_x3w: one 256-column group, A read once per chunk) for
 // the wide hidden layers and for the input layer into a wide layer: rows of A, z_{l+1} (and G_0
@@ -203,9 +196,9 @@ int pgw_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// one layer of the split-fp16 kernel: wide hidden layers one 256-column group of 16 waves
-// (pgx_w_ok), other wide outputs 1 x 8 waves (one column tile each, 128-column groups; see
-// pgx_wide16), outputs of <= 32 columns 8 x 1 waves over the row tiles
+// one layer of the split-fp16 kernel: the wide hidden layers and the input layer one 256-column
+// group of 16 waves (pgx_w_ok), other wide outputs 1 x 8 waves (one column tile each,
+// 128-column groups), outputs of <= 32 columns 8 x 1 waves over the row tiles
 int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   const int K = a.width[l], H = a.width[l + 1];
   const int nti = (K + 15) / 16;
@@ -224,12 +217,6 @@ int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   if (l == 0) {  // the input layer (d <= 32: launch() sends the others to the f32 kernel)
     const dim3 grid((unsigned)nch, (unsigned)((H + 127) / 128));
     return nti <= 1 ? pgx_launch<1, 1, 1, true>(a, l, grid, s) : pgx_launch<2, 1, 1, true>(a, l, grid, s);
-  }
-  if (pgx_wide16()) {
-    const dim3 grid((unsigned)nch, (unsigned)((H + 255) / 256));
-    if (nti <= 4) return pgx_launch<4, 1, 1, false, 16>(a, l, grid, s);
-    if (nti <= 8) return pgx_launch<8, 1, 1, false, 16>(a, l, grid, s);
-    return pgx_launch<13, 1, 1, false, 16>(a, l, grid, s);
   }
   const dim3 grid((unsigned)nch, (unsigned)((H + 127) / 128));
   if (nti <= 1) return pgx_launch<1, 1, 1, false>(a, l, grid, s);

@@ -71,9 +71,9 @@ __device__ __forceinline__ void pgx_split8(const float (&v)[8], pgh8& h, pgh8& l
   }
 }
 
-// The layout of one workgroup of NW wavefronts (8: 512 threads; 16: 1024 threads, one 256-column
-// group for the wide layers, so their A operand is staged once per chunk instead of once per
-// 128-column group).  Shared with the host (dynamic LDS size).
+// The layout of one workgroup of NW wavefronts (8: 512 threads; a 16-wavefront register-staged
+// build spilled, round 4: the wide layers' one-group kernel is k_param_grads_x3w below).
+// Shared with the host (dynamic LDS size).
 template <int NTI, int NTJ, int WI, bool L0, int NW>
 struct PgxPlan {
   static constexpr int kThreads = 64 * NW;

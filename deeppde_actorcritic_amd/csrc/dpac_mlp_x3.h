@@ -47,7 +47,10 @@ typedef float x3f4 __attribute__((ext_vector_type(4)));
 
 constexpr int kX3Waves = 8;
 constexpr int kX3Threads = 64 * kX3Waves;
-constexpr int kX3RT = 4;                  // row tiles per workgroup
+#ifndef DPAC_X3_RT
+#define DPAC_X3_RT 4  // row tiles per workgroup (timing knob)
+#endif
+constexpr int kX3RT = DPAC_X3_RT;         // row tiles per workgroup
 constexpr int kX3Rows = 16 * kX3RT;       // 64 rows
 constexpr int kX3MaxChunks = (DPAC_MLP_MAX_WIDTH + 31) / 32;  // 8
 #ifndef DPAC_X3_LDPAD
