@@ -375,13 +375,13 @@ X3Args x3_args(const dpac_mlp& net, int64_t rows, const void* const* img, const 
   return a;
 }
 
+// one workgroup per `rows_per` rows (the forward's kX3Rows, the backward's kX3RowsB), `lds` bytes
 template <class K>
-int x3_launch(K kfn, const X3Args& a, hipStream_t s) {
+int x3_launch(K kfn, const X3Args& a, hipStream_t s, int rows_per = kX3Rows, uint32_t lds = kX3LdsBytes) {
   if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kX3LdsBytes))
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
     return (int)e;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)((a.rows + kX3Rows - 1) / kX3Rows)), dim3(kX3Threads), kX3LdsBytes, s,
-                     a);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)((a.rows + rows_per - 1) / rows_per)), dim3(kX3Threads), lds, s, a);
   return (int)hipGetLastError();
 }
 
@@ -435,7 +435,7 @@ int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const voi
       a.G = (float*)G;
       a.g_x = (float*)g_x;
       a.status = net.status;
-      if (int e = x3_launch(k_mlp_rows_bwd_x3, a, s)) return e;
+      if (int e = x3_launch(k_mlp_rows_bwd_x3, a, s, kX3RowsB, kX3LdsBytesB)) return e;
       if (!net.status) return 0;
       MrArgs<T> f = mr_args<T>(net, rows);  // the f32 kernel, run only once the x3 kernel fell back
       set_td(f, td);

@@ -48,10 +48,15 @@ typedef float x3f4 __attribute__((ext_vector_type(4)));
 constexpr int kX3Waves = 8;
 constexpr int kX3Threads = 64 * kX3Waves;
 #ifndef DPAC_X3_RT
-#define DPAC_X3_RT 4  // row tiles per workgroup (timing knob)
+#define DPAC_X3_RT 4  // row tiles per workgroup of the forward (timing knob)
 #endif
-constexpr int kX3RT = DPAC_X3_RT;         // row tiles per workgroup
+#ifndef DPAC_X3_RT_BWD
+#define DPAC_X3_RT_BWD 2  // of the backward chain: at 4 it needs > 256 VGPRs and spills 432 B per lane
+#endif
+constexpr int kX3RT = DPAC_X3_RT;         // row tiles per workgroup (forward)
 constexpr int kX3Rows = 16 * kX3RT;       // 64 rows
+constexpr int kX3RTB = DPAC_X3_RT_BWD;    // row tiles per workgroup (backward)
+constexpr int kX3RowsB = 16 * kX3RTB;     // 32 rows
 constexpr int kX3MaxChunks = (DPAC_MLP_MAX_WIDTH + 31) / 32;  // 8
 #ifndef DPAC_X3_LDPAD
 #define DPAC_X3_LDPAD 16  // halves of padding per LDS row (a multiple of 8: 16-byte rows)
@@ -153,7 +158,7 @@ __device__ __forceinline__ x3f4 x3_load4(__amdgpu_buffer_rsrc_t r, const float* 
 // = ceil(K / 32) as a template constant (straight-line code, counted waits) or 0
 // (runtime K, single-buffered).  epi.pre<NT>() runs before the K loop, epi.post<NT>()
 // after it.  Returns whether a stored operand left the split range (epi.store's result).
-template <int NT, int NCH, class EPI>
+template <int NT, int NCH, int RT, class EPI>
 __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, const _Float16* Wx3, int wave,
                                            int lane, EPI& epi) {
   const int col_l = lane & 15, q = lane >> 4;
@@ -161,13 +166,13 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
   const int ntiles = (Nout + 15) / 16;
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wx3, (uint32_t)(ntiles * nch * 2048));
   uint32_t voff[NT];
-  x3f4 ah[kX3RT][NT], al[kX3RT][NT];
+  x3f4 ah[RT][NT], al[RT][NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int tile = wave + kX3Waves * j;
     voff[j] = tile < ntiles ? (uint32_t)(tile * nch * 2048 + 16 * lane) : kOOB;
 #pragma unroll
-    for (int rt = 0; rt < kX3RT; ++rt) ah[rt][j] = al[rt][j] = x3f4{0, 0, 0, 0};
+    for (int rt = 0; rt < RT; ++rt) ah[rt][j] = al[rt][j] = x3f4{0, 0, 0, 0};
   }
   (void)col_l;
   auto loadW = [&](int c, int j, int part) {  // part 0: hi, 1: lo; one contiguous KB per wave
@@ -178,9 +183,9 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
   auto loadX = [&](int c, int rt, int part) {
     return *reinterpret_cast<const x3h8*>(arow + rt * 16 * kX3Ld + c * 64 + 32 * part);
   };
-  auto step = [&](const x3h8 (&wh)[NT], const x3h8 (&wl)[NT], const x3h8 (&xh)[kX3RT], const x3h8 (&xl)[kX3RT]) {
+  auto step = [&](const x3h8 (&wh)[NT], const x3h8 (&wl)[NT], const x3h8 (&xh)[RT], const x3h8 (&xl)[RT]) {
 #pragma unroll
-    for (int rt = 0; rt < kX3RT; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         ah[rt][j] = x3_mma(wh[j], xh[rt], ah[rt][j]);
@@ -199,9 +204,9 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
         wl[f][j] = loadW(f, j, 1);
       }
     epi.template pre<NT>(wave, lane);
-    x3h8 xh[2][kX3RT], xl[2][kX3RT];
+    x3h8 xh[2][RT], xl[2][RT];
 #pragma unroll
-    for (int rt = 0; rt < kX3RT; ++rt) {
+    for (int rt = 0; rt < RT; ++rt) {
       xh[0][rt] = loadX(0, rt, 0);
       xl[0][rt] = loadX(0, rt, 1);
     }
@@ -210,7 +215,7 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
       const int sx = c & 1, sw = c % PF;
       if (c + 1 < NCH) {
 #pragma unroll
-        for (int rt = 0; rt < kX3RT; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
           xh[sx ^ 1][rt] = loadX(c + 1, rt, 0);
           xl[sx ^ 1][rt] = loadX(c + 1, rt, 1);
         }
@@ -230,7 +235,7 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
     }
   } else {
     epi.template pre<NT>(wave, lane);
-    x3h8 wh[NT], wl[NT], xh[kX3RT], xl[kX3RT];
+    x3h8 wh[NT], wl[NT], xh[RT], xl[RT];
     for (int c = 0; c < nch; ++c) {
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
@@ -238,7 +243,7 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
         wl[j] = loadW(c, j, 1);
       }
 #pragma unroll
-      for (int rt = 0; rt < kX3RT; ++rt) {
+      for (int rt = 0; rt < RT; ++rt) {
         xh[rt] = loadX(c, rt, 0);
         xl[rt] = loadX(c, rt, 1);
       }
@@ -252,11 +257,11 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
-    for (int rt = 0; rt < kX3RT; ++rt) bad |= epi.store(j, rt, ah[rt][j] + al[rt][j] * kX3LoInv, wave, lane);
+    for (int rt = 0; rt < RT; ++rt) bad |= epi.store(j, rt, ah[rt][j] + al[rt][j] * kX3LoInv, wave, lane);
   return bad;
 }
 
-template <class EPI>
+template <int RT = kX3RT, class EPI>
 __device__ __forceinline__ bool x3_layer(const _Float16* in, int K, int Nout, const _Float16* Wx3, int wave,
                                          int lane, EPI& epi) {
   const int ntiles = (Nout + 15) / 16;
@@ -264,15 +269,15 @@ __device__ __forceinline__ bool x3_layer(const _Float16* in, int K, int Nout, co
   const int nch = x3_chunks(K);
   // straight-line layers for the shipped shapes (d <= 32: one chunk; 193..224 wide: seven)
   if (nch == 1) {
-    if (mine == 1) return x3_layer_t<1, 1>(in, K, Nout, Wx3, wave, lane, epi);
-    if (mine == 2) return x3_layer_t<2, 1>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 1) return x3_layer_t<1, 1, RT>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 2) return x3_layer_t<2, 1, RT>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (nch == 7) {
-    if (mine == 1) return x3_layer_t<1, 7>(in, K, Nout, Wx3, wave, lane, epi);
-    if (mine == 2) return x3_layer_t<2, 7>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 1) return x3_layer_t<1, 7, RT>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 2) return x3_layer_t<2, 7, RT>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (mine == 1) {
-    return x3_layer_t<1, 0>(in, K, Nout, Wx3, wave, lane, epi);
+    return x3_layer_t<1, 0, RT>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (mine == 2) {
-    return x3_layer_t<2, 0>(in, K, Nout, Wx3, wave, lane, epi);
+    return x3_layer_t<2, 0, RT>(in, K, Nout, Wx3, wave, lane, epi);
   }
   return false;
 }
@@ -365,7 +370,7 @@ struct X3FwdEpi {
 // Backward epilogue of g = G_{l+1} @ (W_l diag s_{l+1})^T: times 1 + [BN_l(z_l) > 0] for
 // l >= 1 (FIRST = false); G_l (unscaled by the row's power of two) to global; scaled and
 // split into LDS; for l == 0 (FIRST) also dL/dx = G_0 * s_0.
-template <bool FIRST>
+template <bool FIRST, int RT = kX3RTB>
 struct X3BwdEpi {
   int mark;                    // trace point of this layer's K loop end (DPAC_X3_TRACE)
   const float *scale, *shift;  // BN_l (l >= 1)
@@ -382,8 +387,8 @@ struct X3BwdEpi {
   const float* zp;             // plain pointers to the same rows (partial quads)
   float *gp, *xp;
   x3f4 s[kX3MaxNT], sh[kX3MaxNT];
-  float ri[kX3RT];
-  x3f4 zz[kX3MaxNT][kX3RT];    // z_l of the lane's quads, loaded in post()
+  float ri[RT];
+  x3f4 zz[kX3MaxNT][RT];    // z_l of the lane's quads, loaded in post()
   template <int NT>
   __device__ __forceinline__ void pre(int wave, int lane) {
 #pragma unroll
@@ -397,7 +402,7 @@ struct X3BwdEpi {
       }
     }
 #pragma unroll
-    for (int rt = 0; rt < kX3RT; ++rt) ri[rt] = rinv[rt * 16 + (lane & 15)];
+    for (int rt = 0; rt < RT; ++rt) ri[rt] = rinv[rt * 16 + (lane & 15)];
   }
   template <int NT>
   __device__ __forceinline__ void post(int wave, int lane) {  // every z load, then one wait
@@ -406,7 +411,7 @@ struct X3BwdEpi {
       for (int j = 0; j < NT; ++j) {
         const int f0 = x3_f0(wave, j, lane), nv = x3_nvalid(f0, Nout);
 #pragma unroll
-        for (int rt = 0; rt < kX3RT; ++rt)
+        for (int rt = 0; rt < RT; ++rt)
           zz[j][rt] = x3_load4(rz, zp, (uint32_t)((rt * 16 + (lane & 15)) * z_ld + f0), nv,
                                rt * 16 + (lane & 15) < rows_live);
       }
@@ -429,9 +434,10 @@ struct X3BwdEpi {
   }
 };
 
+template <int ROWS = kX3Rows>
 __device__ __forceinline__ void x3_zero(_Float16* img, int tid) {
   uint4* p = reinterpret_cast<uint4*>(img);
-  constexpr int n = kX3Rows * kX3Ld * 2 / 16;
+  constexpr int n = ROWS * kX3Ld * 2 / 16;
   for (int e = tid; e < n; e += kX3Threads) p[e] = uint4{0, 0, 0, 0};
 }
 
@@ -440,6 +446,8 @@ __device__ __forceinline__ void x3_zero(_Float16* img, int tid) {
 constexpr uint32_t kX3ImgBytes = kX3Rows * kX3Ld * 2;
 static_assert(kX3Rows * kMrLd * 4 <= kX3ImgBytes, "the f32 staging rows fit in one split image");
 constexpr uint32_t kX3LdsBytes = 2 * kX3ImgBytes + kX3Rows * 4;
+constexpr uint32_t kX3ImgBytesB = kX3RowsB * kX3Ld * 2;  // the backward's (kX3RTB row tiles)
+constexpr uint32_t kX3LdsBytesB = 2 * kX3ImgBytesB + kX3RowsB * 4;
 
 // rows [row0, row0 + live) of a [rows][ld] float array as a buffer descriptor
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t x3_rows_rsrc(const float* base, int64_t row0, int live, int ld) {
@@ -527,27 +535,27 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
 __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char x3_lds[];
   _Float16* const img0 = reinterpret_cast<_Float16*>(x3_lds);
-  _Float16* const img1 = reinterpret_cast<_Float16*>(x3_lds + kX3ImgBytes);
+  _Float16* const img1 = reinterpret_cast<_Float16*>(x3_lds + kX3ImgBytesB);
   auto img = [&](int i) { return i ? img1 : img0; };
-  float* rinv = reinterpret_cast<float*>(x3_lds + 2 * kX3ImgBytes);
+  float* rinv = reinterpret_cast<float*>(x3_lds + 2 * kX3ImgBytesB);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
   if (x3_status_set(a.status)) return;  // fell back: the f32 kernel after this one does the work
-  const int64_t row0 = (int64_t)blockIdx.x * kX3Rows;
-  const int rows_live = (int)((a.rows - row0) < kX3Rows ? (a.rows - row0) : kX3Rows);
+  const int64_t row0 = (int64_t)blockIdx.x * kX3RowsB;
+  const int rows_live = (int)((a.rows - row0) < kX3RowsB ? (a.rows - row0) : kX3RowsB);
   const int L = a.L, hout = a.width[L + 1];
   bool bad = false;
   X3_MARK(0);
   MrArgs<float> ta{};
   ta.td_x = a.td_x; ta.td_u = a.td_u; ta.td_dw = a.td_dw; ta.td_ldx = a.td_ldx; ta.td_ldu = a.td_ldu;
   ta.td_sa = a.td_sa; ta.td_sb = a.td_sb;
-  x3_zero(img0, tid);
-  x3_zero(img1, tid);
+  x3_zero<kX3RowsB>(img0, tid);
+  x3_zero<kX3RowsB>(img1, tid);
   __syncthreads();
   // G_{L+1} = dL/d out, row by row (8 lanes per row): to G unscaled, and times the row's
   // power of two 2^e (max |G_{L+1}| of the row in [1, 2)) split into image 0
   {
-    const int r = tid / 8, sub = tid % 8;  // 512 threads = 64 rows x 8 lanes
+    const int r = tid / 8, sub = tid % 8;  // 8 lanes per row (kX3RowsB rows: the first 8 kX3RowsB threads)
     const bool live = r < rows_live;
     const int64_t gr = row0 + (live ? r : 0);
     float mx = 0.f;
@@ -563,9 +571,9 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
     const float sc = ldexpf(1.f, 1 - e);                   // max |G| * sc in [1, 2)
     for (int k = sub; k < hout; k += 8) {
       const float v = live ? (a.g_gdot ? a.g_gdot[gr] * td_sdw(ta, gr, k, hout) : a.g_out[gr * hout + k]) : 0.f;
-      bad |= x3_put(img0, r, k, v * sc);
+      if (r < kX3RowsB) bad |= x3_put(img0, r, k, v * sc);
     }
-    if (sub == 0) rinv[r] = ldexpf(1.f, e - 1);
+    if (sub == 0 && r < kX3RowsB) rinv[r] = ldexpf(1.f, e - 1);
   }
   __syncthreads();
   X3_MARK(1);
@@ -577,12 +585,12 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
       X3BwdEpi<false> epi{2 + 2 * (L - l), a.scale[l], a.shift[l], rows_live, a.width[l], img(pq ^ 1),
                           x3_rows_rsrc(a.z + a.zoff[l], row0, rows_live, a.ztot), a.ztot, rg, a.gtot,
                           make_rsrc(nullptr, 0), false, nullptr, rinv, a.z + a.zoff[l] + row0 * a.ztot, gp, nullptr};
-      bad |= x3_layer(img(pq), a.width[l + 1], a.width[l], a.wx3[l], wave, lane, epi);
+      bad |= x3_layer<kX3RTB>(img(pq), a.width[l + 1], a.width[l], a.wx3[l], wave, lane, epi);
     } else {
       X3BwdEpi<true> epi{2 + 2 * L, nullptr, nullptr, rows_live, a.width[0], img(pq ^ 1), make_rsrc(nullptr, 0), 0, rg, a.gtot,
                          x3_rows_rsrc(a.g_x, row0, rows_live, a.width[0]), a.g_x != nullptr, a.scale[0], rinv,
                          nullptr, gp, a.g_x ? a.g_x + row0 * a.width[0] : nullptr};
-      x3_layer(img(pq), a.width[1], a.width[0], a.wx3[0], wave, lane, epi);  // dL/dx: not split again
+      x3_layer<kX3RTB>(img(pq), a.width[1], a.width[0], a.wx3[0], wave, lane, epi);  // dL/dx: not split again
     }
     __syncthreads();
     X3_MARK(3 + 2 * (L - l));
