@@ -53,7 +53,7 @@ def main():
         actor()
         iteration()
     torch.cuda.synchronize()
-    tc = ta = ti = 0.0
+    tc = ta = ti = th = 0.0
     for _ in range(a.iters):
         t0 = time.perf_counter()
         critic()
@@ -63,6 +63,7 @@ def main():
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         iteration()
+        th += time.perf_counter() - t2  # the host's submission of the iteration
         torch.cuda.synchronize()
         t3 = time.perf_counter()
         tc += t1 - t0
@@ -72,6 +73,7 @@ def main():
     print(json.dumps({"config": a.config, "dtype": a.dtype, "batch": B, "N": N, "iters": a.iters,
                       "ms_per_iter": ms, "sequential_ms": (tc + ta) / a.iters * 1e3,
                       "critic_ms": tc / a.iters * 1e3, "actor_ms": ta / a.iters * 1e3,
+                      "host_submit_ms": th / a.iters * 1e3,
                       "traj_steps_per_s": 2 * B * N / (ms * 1e-3)}), flush=True)
 
 
