@@ -475,8 +475,13 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
 #ifndef DPAC_ST_TIGHT_CHUNKS
 #define DPAC_ST_TIGHT_CHUNKS 3  // hand-off chunks of a ring of 16-byte-aligned slots
 #endif
+#ifndef DPAC_ST_PD
+#define DPAC_ST_PD 1  // compute waves: steps of dw read from the ring ahead of use
+#endif
 constexpr int kStCW = 4;   // compute wavefronts per workgroup
 constexpr int kStCH = 16;  // steps per hand-off chunk
+constexpr int kStPD = DPAC_ST_PD;
+static_assert(kStPD >= 1 && kStPD <= kStCH, "prefetch distance within a chunk");
 template <typename T, int D, int P>
 struct StagedPlan {
   static constexpr int TPW = kStCW * (64 / P);                                   // trajectories per workgroup
@@ -664,14 +669,17 @@ __global__ __launch_bounds__(64 * (kStCW + 1)) void k_rollout_staged(const E eq,
     if (c0 + kStCH <= N) {
       // RS is a multiple of kStCH: the chunk's slots are contiguous from cb
       const uint32_t cb = (uint32_t)__builtin_amdgcn_readfirstlane((c0 % RS) * SLOT_LDS);
-      T nxt[M];
-      read_dw_at(c0, cb, nxt);
+      constexpr int PD = kStPD;  // steps of dw in registers ahead of use
+      T nxt[PD][M];
+#pragma unroll
+      for (int q = 0; q < PD; ++q) read_dw_at(c0 + q, cb + (uint32_t)(q * SLOT_LDS), nxt[q]);
       auto one = [&](auto sidx) {
         constexpr int S = decltype(sidx)::value;
         T cur[M];
 #pragma unroll
-        for (int m = 0; m < M; ++m) cur[m] = nxt[m];
-        if constexpr (S + 1 < kStCH) read_dw_at(c0 + S + 1, cb + (uint32_t)((S + 1) * SLOT_LDS), nxt);
+        for (int m = 0; m < M; ++m) cur[m] = nxt[S % PD][m];
+        if constexpr (S + PD < kStCH) read_dw_at(c0 + S + PD, cb + (uint32_t)((S + PD) * SLOT_LDS), nxt[S % PD]);
+        if constexpr (PD > 1) __builtin_amdgcn_sched_barrier(0);  // issue the read here, PD steps ahead
         body(c0 + S, cur, Phase<S>{});
       };
       unroll_phases(one, std::make_integer_sequence<int, kStCH>{});
