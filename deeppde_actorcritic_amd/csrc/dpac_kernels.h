@@ -1122,6 +1122,16 @@ inline int nn_tile_rows() {
   return (v == 4 || v == 16) ? v : 0;     // 0: by batch size
 }
 
+// Trajectories per workgroup of the split-fp16 NN kernels (k_rollout_nn_x3, k_rollout_nn_bwd_x3):
+// 16 (one MFMA row tile) or 8 (half a tile, twice the workgroups).  DPAC_NX_ROWS=8 / 16 forces one.
+inline int nx_rows(int64_t B) {
+  const char* e = getenv("DPAC_NX_ROWS");  // read per launch: tests switch it in-process
+  const int v = e ? atoi(e) : 0;
+  if (v == 8 || v == 16) return v;
+  (void)B;
+  return 16;
+}
+
 inline dim3 grid_for(int64_t B, int P) {
   const int64_t per = 64 / P;
   return dim3((unsigned)((B + per - 1) / per));
@@ -1271,12 +1281,13 @@ int run_op(const OpArgs& a) {
         if (r.mask && bptt_kernel() == 2 && (!m.status || r.fast) &&
             nn_x3_host(m.L, m.width, (const void* const*)a.mlp.weight_t_x3, m.width[m.L + 1], m.width[0])) {
           for (int i = 0; i <= m.L; ++i) r.wtx3[i] = (const _Float16*)a.mlp.weight_t_x3[i];
+          r.tr = nx_rows(a.B);
           auto kfn = adaptive ? k_rollout_nn_bwd_x3<E, D, DPAC_SCHEME_ADAPTIVE>
                               : k_rollout_nn_bwd_x3<E, D, DPAC_SCHEME_NAIVE>;
           if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)NxLds::total))
             return (int)e;
-          hipLaunchKernelGGL(kfn, ngrid, nblock, NxLds::total, s, eq, c, m, r);
+          hipLaunchKernelGGL(kfn, dim3((unsigned)((a.B + r.tr - 1) / r.tr)), nblock, NxLds::total, s, eq, c, m, r);
           if (m.status) {  // the f32 BPTT, run only once the x3 kernel fell back (dpac.h dpac_mlp.status)
             int wsum = 0;
             for (int i = 0; i <= m.L + 1; ++i) wsum += m.width[i];
@@ -1395,13 +1406,15 @@ int run_op(const OpArgs& a) {
         if (x3) {
           for (int i = 0; i <= m.L; ++i) m.wx3[i] = (const _Float16*)a.mlp.weight_x3[i];
           const bool save = r.save_z != nullptr, mask = r.save_mask != nullptr;
+          r.tr = nx_rows(a.B);
+          const dim3 xgrid((unsigned)((a.B + r.tr - 1) / r.tr));
           hipError_t e = hipSuccess;
 #define DPAC_NX_LAUNCH(SCH, CO, SV, MK)                                                                    \
   {                                                                                                       \
     auto kfn = k_rollout_nn_x3<E, D, SCH, CO, SV, MK>;                                                    \
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, \
                             (int)NxLds::total);                                                           \
-    if (e == hipSuccess) hipLaunchKernelGGL(kfn, ngrid, nblock, NxLds::total, s, eq, c, m, r);            \
+    if (e == hipSuccess) hipLaunchKernelGGL(kfn, xgrid, nblock, NxLds::total, s, eq, c, m, r);            \
   }
 #define DPAC_NX_SV(SCH, CO)                                    \
   if (mask) DPAC_NX_LAUNCH(SCH, CO, true, true)                \

@@ -94,6 +94,7 @@ struct NnRolloutArgs {
   int mb;               // mask bytes per 16-row tile
   const uint32_t* guard;  // the f32 fallback of a split-fp16 launch: run only once this word
                           // is set (dpac.h dpac_mlp.status); null = always run
+  int tr;               // k_rollout_nn_x3: trajectories per workgroup (16, or 8: half a row tile)
 };
 
 // out[16 x Nout] = in[16 x K] @ W[K x Nout] for the workgroup's 16 rows, this
@@ -878,6 +879,7 @@ struct NnBackArgs {
   int mb;
   const _Float16* wtx3[DPAC_MLP_MAX_HIDDEN + 1];  // split-fp16 images of wt (k_rollout_nn_bwd_x3)
   const uint32_t* guard;  // as NnRolloutArgs::guard
+  int tr;                 // as NnRolloutArgs::tr (k_rollout_nn_bwd_x3)
 };
 
 // The actor's BPTT through a fused NN rollout, as one launch: the reverse time

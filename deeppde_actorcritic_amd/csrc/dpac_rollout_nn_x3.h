@@ -223,7 +223,7 @@ __device__ __forceinline__ int nx_mask_idx(int lane) {  // byte of the tile this
 template <bool SAVE, bool MASK>
 __device__ __forceinline__ bool nx_fwd_epi(const nxf4 (&acc)[2][3], int wave, int lane, int Nout, const float* bn,
                                            _Float16* out, float* zrow0, int ztot, bool zvec, int rows_live,
-                                           uint8_t* mtile) {
+                                           uint8_t* mtile, bool mrow) {
   const int row = lane & 15;
   bool bad = false;
 #pragma unroll
@@ -255,7 +255,7 @@ __device__ __forceinline__ bool nx_fwd_epi(const nxf4 (&acc)[2][3], int wave, in
     bad |= nx_put4(out, kNxLd, row, f0, y);
     if constexpr (MASK && !(DPAC_NX_ABLATE & 2)) {
       const uint32_t w = nx_quad_gather(nib, lane);
-      mtile[64 * tl + nx_mask_idx(lane)] = (uint8_t)nx_pick4(w, lane & 3);
+      if (mrow) mtile[64 * tl + nx_mask_idx(lane)] = (uint8_t)nx_pick4(w, lane & 3);
     }
   }
   return bad;
@@ -346,9 +346,14 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
   bool bad = false;                       // a split operand outside the range (dpac.h dpac_mlp.status)
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
-  const int64_t row0 = (int64_t)blockIdx.x * kNnRows;
-  const int rows_live = (int)((a.B - row0) < kNnRows ? (a.B - row0) : kNnRows);
-  const bool stepper = tid < kNnRows * P;
+  const int tr = a.tr;  // trajectories per workgroup: 16, or 8 (rows 8..15 of the tile stay zero)
+  const int64_t row0 = (int64_t)blockIdx.x * tr;
+  const int rows_live = (int)((a.B - row0) < tr ? (a.B - row0) : tr);
+  const bool stepper = tid < tr * P;
+  // sign-bit mask bytes: a byte holds 4 rows of one feature of a 16-row tile (FwdEpiM's layout);
+  // an 8-row workgroup at row0 % 16 == 8 owns the tile's row groups 2, 3 (+32 bytes)
+  const int moff = (int)(row0 & 15) * 4;
+  const bool mrow = (lane & 15) < tr;
   const int g = stepper ? tid / P : 0;
   const LaneCoord<P> lc(a.B, stepper ? tid % P : 0, row0 + g);
   const bool live = stepper && lc.live;
@@ -420,13 +425,13 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
     __syncthreads();  // a0 of step t is in in0; the previous step's partial reads are done
     NN_MARK(t, 0);
     const int64_t rowt = (int64_t)t * a.B + row0;
-    uint8_t* mt = MASK ? a.save_mask + ((int64_t)t * ntile + (row0 >> 4)) * a.mb : nullptr;
+    uint8_t* mt = MASK ? a.save_mask + ((int64_t)t * ntile + (row0 >> 4)) * a.mb + moff : nullptr;
     {  // hidden layer 1 from a0 (narrow K, resident weights)
       nxf4 acc[2][3];
       nx_prod<1, kNxLd0, 0>(in0, 0, rih, ril, acc, lane);
       bad |= nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[1], s_bn, img(0),
                              SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[1] : nullptr, mlp.ztot, zvec, rows_live,
-                             mt);
+                             mt, mrow);
     }
     NN_MARK(t, 1);
     __syncthreads();
@@ -443,7 +448,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
       nx_loadw<kNxRing>(wh, wl, mlp.wx3[ln], mlp.width[ln + 1], kNxWide, 0, wave, wave + 8, lane);
       bad |= nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[l + 1], s_bn + l * kNxBnLd, img(l),
                              SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[l + 1] : nullptr, mlp.ztot, zvec,
-                             rows_live, MASK ? mt + 13 * 64 * l : nullptr);
+                             rows_live, MASK ? mt + 13 * 64 * l : nullptr, mrow);
       NN_MARK(t, 1 + 2 * l);
       __syncthreads();
       NN_MARK(t, 2 + 2 * l);
@@ -547,9 +552,14 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
   bool bad = false;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
-  const int64_t row0 = (int64_t)blockIdx.x * kNnRows;
-  const int rows_live = (int)((a.B - row0) < kNnRows ? (a.B - row0) : kNnRows);
-  const bool stepper = tid < kNnRows * P;
+  const int tr = a.tr;  // trajectories per workgroup: 16, or 8 (rows 8..15 of the tile stay zero)
+  const int64_t row0 = (int64_t)blockIdx.x * tr;
+  const int rows_live = (int)((a.B - row0) < tr ? (a.B - row0) : tr);
+  const bool stepper = tid < tr * P;
+  // sign-bit mask bytes: a byte holds 4 rows of one feature of a 16-row tile (FwdEpiM's layout);
+  // an 8-row workgroup at row0 % 16 == 8 owns the tile's row groups 2, 3 (+32 bytes)
+  const int moff = (int)(row0 & 15) * 4;
+  const bool mrow = (lane & 15) < tr;
   const int g = stepper ? tid / P : 0;
   const LaneCoord<P> lc(a.B, stepper ? tid % P : 0, row0 + g);
   const bool live = stepper && lc.live;
@@ -603,12 +613,12 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
       pflag = a.flag[rt + lc.b];
       pdisc = a.disc_t[rt + lc.b];
     }
-    const uint8_t* mt = a.mask + ((int64_t)ts * ntile + (row0 >> 4)) * a.mb + nx_mask_idx(lane);
+    const uint8_t* mt = a.mask + ((int64_t)ts * ntile + (row0 >> 4)) * a.mb + moff + nx_mask_idx(lane);
 #pragma unroll
     for (int h = 0; h < DPAC_MLP_MAX_HIDDEN; ++h)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        pmb[h][j] = (h < L && wave + 8 * j < 13) ? (uint32_t)mt[13 * 64 * h + 64 * (wave + 8 * j)] : 0u;
+        pmb[h][j] = (mrow && h < L && wave + 8 * j < 13) ? (uint32_t)mt[13 * 64 * h + 64 * (wave + 8 * j)] : 0u;
   };
   fetch(a.N - 1);
   __syncthreads();  // LDS zeroed

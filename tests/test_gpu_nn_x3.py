@@ -156,3 +156,39 @@ def test_x3_mask_layout_and_bptt(name, d, hidden, B, scheme, monkeypatch):
         worst = max(worst, err)
     print(f"\n[x3 bptt {name} d={d} B={B}] max rel |dG| per block {worst:.2e}")
     assert worst <= TOL_G
+
+
+@pytest.mark.parametrize("name,d,hidden,B,scheme", CASES + [("LQR", 20, (200, 200, 200), 1033, "adaptive")])
+def test_x3_half_tile_workgroups_bitwise(name, d, hidden, B, scheme, monkeypatch):
+    """8 trajectories per workgroup (DPAC_NX_ROWS=8: twice the workgroups, rows 8..15 of each
+    MFMA row tile zero) against 16 (one tile): a row's products never mix rows, so the forward
+    (states, controls, saves, the sign-bit mask of the live rows) and the BPTT's G are bitwise
+    the same; the mask bytes of the two half-tile workgroups of a tile interleave (+32 bytes)."""
+    cfg, eqp, net, _, x0, dw, N, T = _setup(name, d, hidden, B, scheme, 53)
+    sch = SCHEMES[scheme]
+    monkeypatch.delenv("DPAC_NN_TILE", raising=False)
+    monkeypatch.delenv("DPAC_NN_X3", raising=False)
+    params = [p.detach() for p in net.trainable_variables()]
+    L = len(hidden)
+    gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
+    widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+    view, wt, wt_km = ops.mlp_prepare(gam, bet, Ws, b, net.ekn_head, True)
+    g_y = torch.full((B,), 1.0 / B, device=DEV)
+    out, G = {}, {}
+    for rows in ("16", "8"):
+        monkeypatch.setenv("DPAC_NX_ROWS", rows)
+        out[rows] = _fwd(eqp, sch, x0, dw, T, N, view)
+        x, _, _, u, _, _, (z, flag, disc_t, mask) = out[rows]
+        assert mask is not None
+        g_xN, g_disc = torch.ones_like(x[-1]) * 0.01, torch.full_like(g_y, 0.5)
+        G[rows] = ops.G_all(ops._bptt_fused(eqp, sch, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km,
+                                            widths, g_xN, g_disc, g_y, mask)).clone()
+    monkeypatch.delenv("DPAC_NX_ROWS")
+    a, c = out["16"], out["8"]
+    for i in range(6):
+        assert torch.equal(a[i], c[i]), f"forward output {i}"
+    for i in range(3):
+        assert torch.equal(a[6][i], c[6][i]), f"save {i}"
+    assert torch.equal(_bits(a[6][3], N, B, L), _bits(c[6][3], N, B, L))
+    assert torch.isfinite(G["16"]).all()
+    assert torch.equal(G["16"], G["8"])
