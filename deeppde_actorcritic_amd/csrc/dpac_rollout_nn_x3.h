@@ -346,7 +346,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
   bool bad = false;                       // a split operand outside the range (dpac.h dpac_mlp.status)
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
-  const int tr = a.tr;  // trajectories per workgroup: 16, or 8 (rows 8..15 of the tile stay zero)
+  const int tr = a.tr == 8 ? 8 : kNnRows;  // trajectories per workgroup: 16, or 8 (rows 8..15 of the tile stay zero)
   const int64_t row0 = (int64_t)blockIdx.x * tr;
   const int rows_live = (int)((a.B - row0) < tr ? (a.B - row0) : tr);
   const bool stepper = tid < tr * P;
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
   bool bad = false;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
-  const int tr = a.tr;  // trajectories per workgroup: 16, or 8 (rows 8..15 of the tile stay zero)
+  const int tr = a.tr == 8 ? 8 : kNnRows;  // trajectories per workgroup: 16, or 8 (rows 8..15 of the tile stay zero)
   const int64_t row0 = (int64_t)blockIdx.x * tr;
   const int rows_live = (int)((a.B - row0) < tr ? (a.B - row0) : tr);
   const bool stepper = tid < tr * P;
