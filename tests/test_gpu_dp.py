@@ -2,8 +2,8 @@
 
 Launches tests/dp_equality.py as a child process under torch.distributed.run with two gloo
 ranks sharing cuda:0 (RCCL needs one GPU per rank; the box has one).  Each rank runs the
-product solver's train_iteration (HIP graphs, split critic step, three all-reduces per
-iteration) and train(); rank 0 compares parameters, history and the final arrays with a
+product solver's train_iteration (HIP graphs, split critic step, two gradient all-reduces
+per iteration: V's, then the actor's and G's in one exchange) and train(); rank 0 compares parameters, history and the final arrays with a
 single-process run on the whole batch (see that script's docstring).
 """
 import json

@@ -165,6 +165,62 @@ def test_param_grads_merged_group_kernel_bitwise(widths, R, gscale, monkeypatch)
         assert torch.equal(a, c), float((a - c).abs().max())
 
 
+def test_param_grads_merged_group_high_address_words(monkeypatch):
+    """Regression test of round 4's address fault in k_param_grads_x3w (the operand rows'
+    global_load_lds_dwordx4 takes a wave-uniform row address built from two readfirstlane
+    halves; its first build sign-extended the low word, so any row whose address had bit 31
+    set was loaded from an address 2^32·(2^32-1) off).  Operands are placed by hand inside
+    one 4.5 GiB allocation: x and G where every row's low address word is >= 2^31, and z
+    (read by LDS-DMA both as a layer's A and as the BN sums' operand) straddling a 4 GiB
+    boundary, so its rows have low words just below 2^32 and then just above 0 with the high
+    word carried.  The gradients must equal, bit for bit, those of the same kernel on
+    ordinarily placed copies and those of the two-group kernels (DPAC_PGX_W=0), and lie within
+    the split-fp16 tolerance of the exact-f32 kernel."""
+    widths, R = (20, 200, 200, 200, 20), 20000
+    scales, shifts, Ws, b = random_net(widths, torch.float32, seed=4242)
+    g = torch.Generator().manual_seed(4243)
+    rnd = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(torch.float32).to(DEV)
+    x, z, G = rnd(R, widths[0]), rnd(R, sum(widths[1:])), rnd(R, sum(widths))
+    buf = torch.empty(int(4.5 * 2 ** 30), dtype=torch.uint8, device=DEV)
+    base, span = buf.data_ptr(), buf.numel()
+
+    def place(addr, t):
+        off = addr - base
+        n = t.numel() * 4
+        assert off % 256 == 0 and 0 <= off and off + n <= span
+        v = buf[off:off + n].view(torch.float32).view(t.shape)
+        v.copy_(t)
+        return v
+    k = ((base + 2 ** 32 - 1) >> 32) << 32  # the first 4 GiB boundary inside the allocation
+    assert base <= k < base + span
+    zn = z.numel() * 4
+    zh = place(k - ((zn // 2) // 256) * 256, z)  # straddles k
+    hi_start = k - 2 ** 31 + 4096 if k - 2 ** 31 >= base else k + 2 ** 31 + 4096
+    xh = place(hi_start, x)
+    gh = place(hi_start + ((x.numel() * 4 + 4095) // 4096) * 4096, G)
+    lo_words = [(t.data_ptr() + r * t.stride(0) * 4) & 0xFFFFFFFF for t in (xh, gh) for r in (0, R - 1)]
+    assert all(w >= 2 ** 31 for w in lo_words)
+    assert (zh.data_ptr() >> 32) != ((zh.data_ptr() + zn - 4) >> 32)
+    view = ops.MlpView(scales, shifts, Ws, b, False, weights_x3=[_x3_image(W) for W in Ws])
+    like = scales + shifts + Ws + [b]
+    monkeypatch.delenv("DPAC_PG_X3", raising=False)
+    monkeypatch.delenv("DPAC_PGX_W", raising=False)
+    high = ops.mlp_param_grads(view, xh, zh, gh, like)
+    plain = ops.mlp_param_grads(view, x, z, G, like)
+    monkeypatch.setenv("DPAC_PGX_W", "0")
+    two = ops.mlp_param_grads(view, xh, zh, gh, like)
+    monkeypatch.setenv("DPAC_PG_X3", "0")
+    f32 = ops.mlp_param_grads(view, xh, zh, gh, like)
+    torch.cuda.synchronize()
+    for a, p, c, e in zip(high, plain, two, f32):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, p), float((a - p).abs().max())
+        assert torch.equal(a, c), float((a - c).abs().max())
+        top = float(e.abs().max())
+        assert float((a - e).abs().max()) <= 2e-5 * top + 1e-30
+    del buf
+
+
 def test_param_grads_strided_input_and_bad_args():
     widths = (20, 64, 20)
     scales, shifts, Ws, b = random_net(widths, torch.float64, seed=5)
