@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPAC_LIB", os.path.join(_HERE, "libdpac.so"))
 
 # constants mirrored from include/dpac.h
-ABI_VERSION = 6  # DPAC_ABI_VERSION: load() refuses a library built from another header
+ABI_VERSION = 7  # DPAC_ABI_VERSION: load() refuses a library built from another header
 DPAC_OK, DPAC_EINVAL, DPAC_EUNSUP = 0, -1, -2
 F32, F64 = 0, 1
 EQN_LQR, EQN_VDP, EQN_EKN, EQN_LQR_VAR = 0, 1, 2, 3
@@ -112,6 +112,14 @@ SIGNATURES = {
     "dpac_mlp_rows_fwd_td1": [_EQ, _I32, _I64, ctypes.POINTER(Mlp), _P, _I64, _P, _P, _P, _P, _P],
     "dpac_mlp_rows_bwd_td1": [_EQ, _I32, _I64, ctypes.POINTER(Mlp), ctypes.POINTER(ctypes.c_void_p),
                               ctypes.POINTER(ctypes.c_void_p), _P, _P, _I64, _P, _P, _P, _P, _P, _P],
+    "dpac_mlp_rows_mask_bytes": [ctypes.POINTER(Mlp), _I32, _I64],
+    "dpac_mlp_rows_fwd_masked": [_I32, _I64, ctypes.POINTER(Mlp), _P, _I64, _P, _P, _P, ctypes.POINTER(_I32), _P],
+    "dpac_mlp_rows_bwd_masked": [_I32, _I64, ctypes.POINTER(Mlp), ctypes.POINTER(ctypes.c_void_p),
+                                 ctypes.POINTER(ctypes.c_void_p), _P, _P, _P, _P, _P, _P],
+    "dpac_mlp_rows_fwd_td1_masked": [_EQ, _I32, _I64, ctypes.POINTER(Mlp), _P, _I64, _P, _P, _P, _P, _P,
+                                     ctypes.POINTER(_I32), _P],
+    "dpac_mlp_rows_bwd_td1_masked": [_EQ, _I32, _I64, ctypes.POINTER(Mlp), ctypes.POINTER(ctypes.c_void_p),
+                                     ctypes.POINTER(ctypes.c_void_p), _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
     "dpac_mlp_param_grads_workspace": [_I32, _I64, ctypes.POINTER(Mlp)],
     "dpac_mlp_param_grads": [_I32, _I64, ctypes.POINTER(Mlp), _D, _P, _I64, _P, _P, _P, _I64, _P,
                              _P],
@@ -123,7 +131,8 @@ SIGNATURES = {
 }
 _RESTYPES = {"dpac_abi_version": ctypes.c_int32, "dpac_last_error": ctypes.c_char_p,
              "dpac_supported": ctypes.c_int32, "dpac_mlp_param_grads_workspace": ctypes.c_int64,
-             "dpac_rollout_nn_mask_tile_bytes": ctypes.c_int32, "dpac_rollout_nn_mask_bytes": ctypes.c_int64}
+             "dpac_rollout_nn_mask_tile_bytes": ctypes.c_int32, "dpac_rollout_nn_mask_bytes": ctypes.c_int64,
+             "dpac_mlp_rows_mask_bytes": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None

@@ -24,10 +24,12 @@ int mlp_param_grads_launch(int dtype, int64_t rows, const dpac_mlp& net, double 
                            const void* x, int64_t ldx, const void* z, const void* G, void* ws,
                            void* out, hipStream_t s);
 int mlp_rows_fwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx,
-                        void* out, void* save_z, const TdRows* td, hipStream_t s);
-int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
-                        const void* save_z, const void* g_out, void* G, void* g_x, const TdRows* td,
+                        void* out, void* save_z, const TdRows* td, uint8_t* mask, int32_t* written,
                         hipStream_t s);
+int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
+                        const void* save_z, const uint8_t* mask, const void* g_out, void* G, void* g_x,
+                        const TdRows* td, hipStream_t s);
+int64_t mlp_rows_mask_bytes(int dtype, int64_t rows, const dpac_mlp& net);
 int mlp_prepare_launch(int dtype, const dpac_mlp& net, double gamma_scale, void* scales, void* wt,
                        void* wkm, void* wtkm, void* wx3, void* wtx3, hipStream_t s);
 int critic_loss_launch(int dtype, int64_t B, const void* V, const void* y, const void* disc, const void* zb,
@@ -471,8 +473,23 @@ int dpac_rollout_nn_bwd_masked(const dpac_eqn_params* eq, int32_t scheme, int32_
   return launch(a);
 }
 
+int64_t dpac_mlp_rows_mask_bytes(const dpac_mlp* net, int32_t dtype, int64_t rows) {
+  if (check_net(net)) return -1;
+  if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype), -1;
+  if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1"), -1;
+  ok();
+  return mlp_rows_mask_bytes(dtype, rows, *net);
+}
+
 int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* x,
                       int64_t ldx, void* out, void* save_z, void* stream) {
+  return dpac_mlp_rows_fwd_masked(dtype, rows, net, x, ldx, out, save_z, nullptr, nullptr, stream);
+}
+
+int dpac_mlp_rows_fwd_masked(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* x,
+                             int64_t ldx, void* out, void* save_z, uint8_t* save_mask,
+                             int32_t* mask_written, void* stream) {
+  if (mask_written) *mask_written = 0;
   if (int e = check_net(net)) return e;
   if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
   if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1 (got %lld)", (long long)rows);
@@ -482,7 +499,9 @@ int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
     if (!net->weight[i]) return fail(DPAC_EINVAL, "weight[%d] is NULL", i);
   DPAC_REQUIRE(x);
   DPAC_REQUIRE(out);
-  const int r = mlp_rows_fwd_launch(dtype, rows, *net, x, ldx, out, save_z, nullptr, (hipStream_t)stream);
+  if (save_mask && !save_z) return fail(DPAC_EINVAL, "save_mask needs save_z");
+  const int r = mlp_rows_fwd_launch(dtype, rows, *net, x, ldx, out, save_z, nullptr, save_mask, mask_written,
+                                    (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();
 }
@@ -490,6 +509,13 @@ int dpac_mlp_rows_fwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
 int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* const* weight_t,
                       const void* const* weight_t_km, const void* save_z, const void* g_out, void* G,
                       void* g_x, void* stream) {
+  return dpac_mlp_rows_bwd_masked(dtype, rows, net, weight_t, weight_t_km, save_z, nullptr, g_out, G, g_x,
+                                  stream);
+}
+
+int dpac_mlp_rows_bwd_masked(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* const* weight_t,
+                             const void* const* weight_t_km, const void* save_z, const uint8_t* save_mask,
+                             const void* g_out, void* G, void* g_x, void* stream) {
   if (int e = check_net(net)) return e;
   if (dtype != DPAC_F32 && dtype != DPAC_F64) return fail(DPAC_EINVAL, "bad dtype %d", dtype);
   if (rows < 1) return fail(DPAC_EINVAL, "rows must be >= 1 (got %lld)", (long long)rows);
@@ -501,7 +527,7 @@ int dpac_mlp_rows_bwd(int32_t dtype, int64_t rows, const dpac_mlp* net, const vo
     if (!weight_t[i]) return fail(DPAC_EINVAL, "weight_t[%d] is NULL", i);
   dpac_mlp bnet = *net;  // the struct's weight_km (forward images) never reach the backward
   for (int i = 0; i <= net->n_hidden; ++i) bnet.weight_km[i] = weight_t_km ? weight_t_km[i] : nullptr;
-  const int r = mlp_rows_bwd_launch(dtype, rows, bnet, weight_t, save_z, g_out, G, g_x, nullptr,
+  const int r = mlp_rows_bwd_launch(dtype, rows, bnet, weight_t, save_z, save_mask, g_out, G, g_x, nullptr,
                                     (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();
@@ -537,6 +563,14 @@ static int td_rows_setup(const dpac_eqn_params* eq, int32_t dtype, int64_t rows,
 int dpac_mlp_rows_fwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows, const dpac_mlp* net,
                           const void* x, int64_t ldx, const void* u, const void* dw, void* gdot,
                           void* save_z, void* stream) {
+  return dpac_mlp_rows_fwd_td1_masked(eq, dtype, rows, net, x, ldx, u, dw, gdot, save_z, nullptr, nullptr,
+                                      stream);
+}
+
+int dpac_mlp_rows_fwd_td1_masked(const dpac_eqn_params* eq, int32_t dtype, int64_t rows, const dpac_mlp* net,
+                                 const void* x, int64_t ldx, const void* u, const void* dw, void* gdot,
+                                 void* save_z, uint8_t* save_mask, int32_t* mask_written, void* stream) {
+  if (mask_written) *mask_written = 0;
   dpac::TdRows td{};
   if (int e = td_rows_setup(eq, dtype, rows, net, td)) return e;
   if (ldx < eq->dim) return fail(DPAC_EINVAL, "ldx (%lld) < dim (%d)", (long long)ldx, eq->dim);
@@ -546,8 +580,10 @@ int dpac_mlp_rows_fwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows
   DPAC_REQUIRE(dw);
   DPAC_REQUIRE(gdot);
   if (td.sb != 0.0) DPAC_REQUIRE(u);
+  if (save_mask && !save_z) return fail(DPAC_EINVAL, "save_mask needs save_z");
   td.x = x; td.ldx = ldx; td.u = u; td.dw = dw; td.gdot = gdot;
-  const int r = mlp_rows_fwd_launch(dtype, rows, *net, x, ldx, nullptr, save_z, &td, (hipStream_t)stream);
+  const int r = mlp_rows_fwd_launch(dtype, rows, *net, x, ldx, nullptr, save_z, &td, save_mask, mask_written,
+                                    (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();
 }
@@ -556,6 +592,15 @@ int dpac_mlp_rows_bwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows
                           const void* const* weight_t, const void* const* weight_t_km,
                           const void* save_z, const void* x, int64_t ldx, const void* u,
                           const void* dw, const void* g_gdot, void* G, void* g_x, void* stream) {
+  return dpac_mlp_rows_bwd_td1_masked(eq, dtype, rows, net, weight_t, weight_t_km, save_z, nullptr, x, ldx, u,
+                                      dw, g_gdot, G, g_x, stream);
+}
+
+int dpac_mlp_rows_bwd_td1_masked(const dpac_eqn_params* eq, int32_t dtype, int64_t rows, const dpac_mlp* net,
+                                 const void* const* weight_t, const void* const* weight_t_km,
+                                 const void* save_z, const uint8_t* save_mask, const void* x, int64_t ldx,
+                                 const void* u, const void* dw, const void* g_gdot, void* G, void* g_x,
+                                 void* stream) {
   dpac::TdRows td{};
   if (int e = td_rows_setup(eq, dtype, rows, net, td)) return e;
   if (ldx < eq->dim) return fail(DPAC_EINVAL, "ldx (%lld) < dim (%d)", (long long)ldx, eq->dim);
@@ -571,7 +616,7 @@ int dpac_mlp_rows_bwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows
   dpac_mlp bnet = *net;
   for (int i = 0; i <= net->n_hidden; ++i) bnet.weight_km[i] = weight_t_km ? weight_t_km[i] : nullptr;
   td.x = x; td.ldx = ldx; td.u = u; td.dw = dw; td.g_gdot = g_gdot;
-  const int r = mlp_rows_bwd_launch(dtype, rows, bnet, weight_t, save_z, nullptr, G, g_x, &td,
+  const int r = mlp_rows_bwd_launch(dtype, rows, bnet, weight_t, save_z, save_mask, nullptr, G, g_x, &td,
                                     (hipStream_t)stream);
   if (r != 0) return fail(r, "kernel launch failed: %s", hipGetErrorString((hipError_t)r));
   return ok();

@@ -362,6 +362,10 @@ X3Args x3_args(const dpac_mlp& net, int64_t rows, const void* const* img, const 
   a.bias = m.bias;
   a.ztot = m.ztot;
   a.gtot = m.gtot;
+  for (int h = 1, q = 0; h <= a.L + 1; ++h) {  // the sign-bit bytes' quad rows per hidden layer
+    a.mqoff[h] = q;
+    if (h <= a.L) q += (a.width[h] + 3) / 4;
+  }
   if (td) {
     a.td_x = (const float*)td->x;
     a.td_ldx = td->ldx;
@@ -391,7 +395,8 @@ constexpr int64_t kFallbackBlocks = 512;
 
 template <typename T>
 int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void* out,
-             void* save_z, const TdRows* td, hipStream_t s) {
+             void* save_z, const TdRows* td, uint8_t* mask, int32_t* written, hipStream_t s) {
+  if (written) *written = 0;
   MrArgs<T> a = mr_args<T>(net, rows);
   set_td(a, td);
   if (td) a.gdot = (T*)td->gdot;
@@ -411,7 +416,9 @@ int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void
       xa.out = (float*)out;
       xa.z = (float*)save_z;
       xa.status = net.status;
+      xa.mask = save_z ? mask : nullptr;
       if (int e = x3_launch(k_mlp_rows_fwd_x3, xa, s)) return e;
+      if (written && xa.mask) *written = 1;
       if (!net.status) return 0;
       a.guard = net.status;  // the f32 kernel recomputes everything once the x3 kernel fell back
       hipLaunchKernelGGL(k_mlp_rows_fwd<T>, dim3((unsigned)std::min(nblk, kFallbackBlocks)), dim3(kMrThreads), 0,
@@ -425,7 +432,7 @@ int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void
 
 template <typename T>
 int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const void* save_z,
-             const void* g_out, void* G, void* g_x, const TdRows* td, hipStream_t s) {
+             const uint8_t* mask, const void* g_out, void* G, void* g_x, const TdRows* td, hipStream_t s) {
   if constexpr (std::is_same<T, float>::value) {
     if (x3_all(net, net.weight_t_x3) && (!net.status || x3_all(net, wt))) {
       X3Args a = x3_args(net, rows, net.weight_t_x3, td);
@@ -435,7 +442,10 @@ int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const voi
       a.G = (float*)G;
       a.g_x = (float*)g_x;
       a.status = net.status;
-      if (int e = x3_launch(k_mlp_rows_bwd_x3, a, s, kX3RowsB, kX3LdsBytesB)) return e;
+      a.mask = const_cast<uint8_t*>(mask);
+      if (int e = mask ? x3_launch(k_mlp_rows_bwd_x3<true>, a, s, kX3RowsB, kX3LdsBytesB)
+                       : x3_launch(k_mlp_rows_bwd_x3<false>, a, s, kX3RowsB, kX3LdsBytesB))
+        return e;
       if (!net.status) return 0;
       MrArgs<T> f = mr_args<T>(net, rows);  // the f32 kernel, run only once the x3 kernel fell back
       set_td(f, td);
@@ -469,16 +479,24 @@ int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const voi
 }  // namespace
 
 int mlp_rows_fwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx,
-                        void* out, void* save_z, const TdRows* td, hipStream_t s) {
-  return dtype == DPAC_F64 ? rows_fwd<double>(rows, net, x, ldx, out, save_z, td, s)
-                           : rows_fwd<float>(rows, net, x, ldx, out, save_z, td, s);
+                        void* out, void* save_z, const TdRows* td, uint8_t* mask, int32_t* written,
+                        hipStream_t s) {
+  return dtype == DPAC_F64 ? rows_fwd<double>(rows, net, x, ldx, out, save_z, td, nullptr, written, s)
+                           : rows_fwd<float>(rows, net, x, ldx, out, save_z, td, mask, written, s);
 }
 
 int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void* const* wt,
-                        const void* save_z, const void* g_out, void* G, void* g_x, const TdRows* td,
-                        hipStream_t s) {
-  return dtype == DPAC_F64 ? rows_bwd<double>(rows, net, wt, save_z, g_out, G, g_x, td, s)
-                           : rows_bwd<float>(rows, net, wt, save_z, g_out, G, g_x, td, s);
+                        const void* save_z, const uint8_t* mask, const void* g_out, void* G, void* g_x,
+                        const TdRows* td, hipStream_t s) {
+  return dtype == DPAC_F64 ? rows_bwd<double>(rows, net, wt, save_z, nullptr, g_out, G, g_x, td, s)
+                           : rows_bwd<float>(rows, net, wt, save_z, mask, g_out, G, g_x, td, s);
+}
+
+int64_t mlp_rows_mask_bytes(int dtype, int64_t rows, const dpac_mlp& net) {
+  if (dtype != DPAC_F32 || !x3_all(net, net.weight_x3)) return 0;  // only the split-fp16 forward writes it
+  int64_t q = 0;
+  for (int h = 1; h <= net.n_hidden; ++h) q += (net.width[h] + 3) / 4;
+  return q * rows;
 }
 
 int64_t mlp_param_grads_ws_bytes(int dtype, int64_t rows, const dpac_mlp& net) {

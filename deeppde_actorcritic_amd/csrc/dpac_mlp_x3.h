@@ -307,6 +307,11 @@ struct X3Args {
   float* gdot;
   const float* g_gdot;
   uint32_t* status;  // the range guard (dpac_mlp.status), or null
+  // the hidden activations' sign bits (dpac.h dpac_mlp_rows_fwd_masked): byte (mqoff[h] + q) *
+  // rows + r holds bit e = [BN_h(z_h)[r][4 q + e] > 0]; written by the forward, read by the
+  // backward instead of z (null: not written / z read)
+  uint8_t* mask;
+  int mqoff[DPAC_MLP_MAX_HIDDEN + 2];
 };
 
 // the lane's feature quad f0 = 16 tile + 4 (l >> 4) and how many of its features exist
@@ -328,6 +333,8 @@ struct X3FwdEpi {
   int z_ld;                  // floats
   __amdgpu_buffer_rsrc_t ro; // out: the workgroup's rows
   float *zp, *op;            // the same rows as plain pointers (x3_store4's partial quads)
+  uint8_t* mp;               // hidden: the layer's sign-bit bytes at the workgroup's first row, or null
+  int64_t mld;               // bytes between a quad's rows and the next quad's (= rows)
   x3f4 s[kX3MaxNT], sh[kX3MaxNT], bb[kX3MaxNT];
   template <int NT>
   __device__ __forceinline__ void pre(int wave, int lane) {
@@ -353,8 +360,13 @@ struct X3FwdEpi {
     if (MODE != kX3Hidden) y = y + bb[j];  // addmm(b, y, W) (solver.py:270)
     y = sh[j] + y * s[j];                  // addcmul(beta, y, gamma/sqrt(1+eps))
     if (MODE == kX3Hidden) {
+      uint32_t nib = 0;  // the sign bits the backward's activation factor needs (MASKED)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = e < nv ? y[e] + fmaxf(y[e], 0.f) : 0.f;  // y + relu(y) (solver.py:269)
+      for (int e = 0; e < 4; ++e) {
+        nib |= (e < nv && y[e] > 0.f) ? 1u << e : 0u;
+        y[e] = e < nv ? y[e] + fmaxf(y[e], 0.f) : 0.f;  // y + relu(y) (solver.py:269)
+      }
+      if (mp && row < rows_live && nv > 0) mp[(int64_t)(f0 >> 2) * mld + row] = (uint8_t)nib;
       return x3_put4(img, row, f0, y);
     } else if (MODE == kX3Stage) {
 #pragma unroll
@@ -368,9 +380,10 @@ struct X3FwdEpi {
 };
 
 // Backward epilogue of g = G_{l+1} @ (W_l diag s_{l+1})^T: times 1 + [BN_l(z_l) > 0] for
-// l >= 1 (FIRST = false); G_l (unscaled by the row's power of two) to global; scaled and
-// split into LDS; for l == 0 (FIRST) also dL/dx = G_0 * s_0.
-template <bool FIRST, int RT = kX3RTB>
+// l >= 1 (FIRST = false), the sign from the forward's saved z or (MASKED) from its sign-bit
+// bytes; G_l (unscaled by the row's power of two) to global; scaled and split into LDS; for
+// l == 0 (FIRST) also dL/dx = G_0 * s_0.
+template <bool FIRST, bool MASKED = false, int RT = kX3RTB>
 struct X3BwdEpi {
   int mark;                    // trace point of this layer's K loop end (DPAC_X3_TRACE)
   const float *scale, *shift;  // BN_l (l >= 1)
@@ -386,9 +399,12 @@ struct X3BwdEpi {
   const float* rinv;           // LDS: 2^-e of each row (undoes the chain's row scale)
   const float* zp;             // plain pointers to the same rows (partial quads)
   float *gp, *xp;
+  const uint8_t* mp;           // MASKED: layer l's sign-bit bytes at the workgroup's first row
+  int64_t mld;                 // MASKED: bytes between quads (= rows)
   x3f4 s[kX3MaxNT], sh[kX3MaxNT];
   float ri[RT];
-  x3f4 zz[kX3MaxNT][RT];    // z_l of the lane's quads, loaded in post()
+  x3f4 zz[MASKED ? 1 : kX3MaxNT][MASKED ? 1 : RT];  // z_l of the lane's quads, loaded in post()
+  uint32_t mb[MASKED ? kX3MaxNT : 1][MASKED ? RT : 1];  // MASKED: their sign nibbles
   template <int NT>
   __device__ __forceinline__ void pre(int wave, int lane) {
 #pragma unroll
@@ -406,7 +422,17 @@ struct X3BwdEpi {
   }
   template <int NT>
   __device__ __forceinline__ void post(int wave, int lane) {  // every z load, then one wait
-    if constexpr (!FIRST) {
+    if constexpr (!FIRST && MASKED) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int f0 = x3_f0(wave, j, lane), nv = x3_nvalid(f0, Nout);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const int row = rt * 16 + (lane & 15);
+          mb[j][rt] = (nv > 0 && row < rows_live) ? (uint32_t)mp[(int64_t)(f0 >> 2) * mld + row] : 0u;
+        }
+      }
+    } else if constexpr (!FIRST) {
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int f0 = x3_f0(wave, j, lane), nv = x3_nvalid(f0, Nout);
@@ -420,7 +446,10 @@ struct X3BwdEpi {
   __device__ __forceinline__ bool store(int j, int rt, x3f4 v, int wave, int lane) {
     const int f0 = x3_f0(wave, j, lane), nv = x3_nvalid(f0, Nout);
     const int row = rt * 16 + (lane & 15);
-    if constexpr (!FIRST) {
+    if constexpr (!FIRST && MASKED) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = v[e] * (((mb[j][rt] >> e) & 1u) ? 2.f : 1.f);  // d(y + relu(y))/dy
+    } else if constexpr (!FIRST) {
       const x3f4 y = sh[j] + zz[j][rt] * s[j];  // the forward's BN_l output
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = v[e] * (y[e] > 0.f ? 2.f : 1.f);  // d(y + relu(y))/dy
@@ -504,17 +533,18 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
     float* zp = a.z ? a.z + a.zoff[l + 1] + row0 * a.ztot : nullptr;
     if (l < a.L) {
       X3FwdEpi<kX3Hidden> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], nullptr, rows_live, Nout, img(pq ^ 1),
-                              nullptr, rz, a.z != nullptr, a.ztot, make_rsrc(nullptr, 0), zp, nullptr};
+                              nullptr, rz, a.z != nullptr, a.ztot, make_rsrc(nullptr, 0), zp, nullptr,
+                              a.mask ? a.mask + (int64_t)a.mqoff[l + 1] * a.rows + row0 : nullptr, a.rows};
       bad |= x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     } else if (a.gdot) {
       X3FwdEpi<kX3Stage> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], a.bias, rows_live, Nout, nullptr,
                              reinterpret_cast<float*>(img(pq ^ 1)), rz, a.z != nullptr, a.ztot, make_rsrc(nullptr, 0),
-                             zp, nullptr};
+                             zp, nullptr, nullptr, 0};
       x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     } else {
       X3FwdEpi<kX3Out> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], a.bias, rows_live, Nout, nullptr, nullptr,
                            rz, a.z != nullptr, a.ztot, x3_rows_rsrc(a.out, row0, rows_live, Nout), zp,
-                           a.out + row0 * Nout};
+                           a.out + row0 * Nout, nullptr, 0};
       x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     }
     __syncthreads();
@@ -532,6 +562,8 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
   if (bad) x3_flag(a.status);
 }
 
+// MASKED: the activation factors from the forward's sign-bit bytes (a.mask) instead of z
+template <bool MASKED>
 __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char x3_lds[];
   _Float16* const img0 = reinterpret_cast<_Float16*>(x3_lds);
@@ -582,14 +614,16 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
     const __amdgpu_buffer_rsrc_t rg = x3_rows_rsrc(a.G + a.goff[l], row0, rows_live, a.gtot);
     float* gp = a.G + a.goff[l] + row0 * a.gtot;
     if (l >= 1) {
-      X3BwdEpi<false> epi{2 + 2 * (L - l), a.scale[l], a.shift[l], rows_live, a.width[l], img(pq ^ 1),
-                          x3_rows_rsrc(a.z + a.zoff[l], row0, rows_live, a.ztot), a.ztot, rg, a.gtot,
-                          make_rsrc(nullptr, 0), false, nullptr, rinv, a.z + a.zoff[l] + row0 * a.ztot, gp, nullptr};
+      X3BwdEpi<false, MASKED> epi{2 + 2 * (L - l), a.scale[l], a.shift[l], rows_live, a.width[l], img(pq ^ 1),
+                                  x3_rows_rsrc(MASKED ? nullptr : a.z + a.zoff[l], row0, rows_live, a.ztot), a.ztot,
+                                  rg, a.gtot, make_rsrc(nullptr, 0), false, nullptr, rinv,
+                                  a.z + a.zoff[l] + row0 * a.ztot, gp, nullptr,
+                                  MASKED ? a.mask + (int64_t)a.mqoff[l] * a.rows + row0 : nullptr, a.rows};
       bad |= x3_layer<kX3RTB>(img(pq), a.width[l + 1], a.width[l], a.wx3[l], wave, lane, epi);
     } else {
       X3BwdEpi<true> epi{2 + 2 * L, nullptr, nullptr, rows_live, a.width[0], img(pq ^ 1), make_rsrc(nullptr, 0), 0, rg, a.gtot,
                          x3_rows_rsrc(a.g_x, row0, rows_live, a.width[0]), a.g_x != nullptr, a.scale[0], rinv,
-                         nullptr, gp, a.g_x ? a.g_x + row0 * a.width[0] : nullptr};
+                         nullptr, gp, a.g_x ? a.g_x + row0 * a.width[0] : nullptr, nullptr, 0};
       x3_layer<kX3RTB>(img(pq), a.width[1], a.width[0], a.wx3[0], wave, lane, epi);  // dL/dx: not split again
     }
     __syncthreads();

@@ -155,6 +155,10 @@ class MlpView:
     def scales(self):
         return self.tensors[:len(self.widths)]
 
+    @property
+    def shifts(self):
+        return self.tensors[len(self.widths):2 * len(self.widths)]
+
 
 # "on": float networks also get the k-major weight images (dpac_mlp.weight_km) the fused
 # rollout / BPTT read with 4 k per load; "off": the row-major path (test reference).
@@ -544,9 +548,25 @@ def _split_params(params):
     return L, params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
 
 
-def mlp_rows(view: MlpView, x: torch.Tensor, save: bool = False):
+# The row kernels' sign-bit mask (dpac.h dpac_mlp_rows_*_masked, round 5): the split-fp16
+# forward records whether each hidden BN output is positive, and the backward chain reads
+# those bits instead of z (bitwise the same G).  DPAC_ROW_MASK=0: z everywhere.
+ROW_MASK = os.environ.get("DPAC_ROW_MASK", "1") != "0"
+
+
+def _row_mask_buffer(view: MlpView, x: torch.Tensor):
+    """The sign-bit mask buffer the masked row forward fills for x's rows, or None where no
+    mask is written (float64, no split-fp16 images)."""
+    nb = _lib.load().dpac_mlp_rows_mask_bytes(ctypes.byref(view.struct), _dtype_id(x), x.shape[0])
+    if nb < 0:
+        raise _lib.DpacError("dpac_mlp_rows_mask_bytes", int(nb), _lib.load().dpac_last_error().decode())
+    return torch.empty(int(nb), dtype=torch.uint8, device=x.device) if nb > 0 else None
+
+
+def mlp_rows(view: MlpView, x: torch.Tensor, save: bool = False, mask: bool = False):
     """out [R, w_out] (the network before any Eikonal head) for every row of x [R, d],
-    one dpac_mlp_rows_fwd launch; with save=True also z [R, Σ widths[1:]]."""
+    one dpac_mlp_rows_fwd launch; with save=True also z [R, Σ widths[1:]].  With mask=True
+    (and save) returns (out, z, sign-bit mask or None where the kernel wrote none)."""
     _require_gpu(x, *view.tensors)
     _check_same(x, *view.tensors)
     if x.dim() != 2 or x.stride(1) != 1:
@@ -554,8 +574,13 @@ def mlp_rows(view: MlpView, x: torch.Tensor, save: bool = False):
     R = x.shape[0]
     out = torch.empty(R, view.widths[-1], dtype=x.dtype, device=x.device)
     z = torch.empty(R, sum(view.widths[1:]), dtype=x.dtype, device=x.device) if save else None
-    call("dpac_mlp_rows_fwd", _dtype_id(x), R, ctypes.byref(view.struct),
-         ctypes.c_void_p(x.data_ptr()), x.stride(0), _ptr(out), _ptr(z), _stream(x))
+    m = _row_mask_buffer(view, x) if (save and mask) else None
+    written = ctypes.c_int32(0)
+    call("dpac_mlp_rows_fwd_masked", _dtype_id(x), R, ctypes.byref(view.struct),
+         ctypes.c_void_p(x.data_ptr()), x.stride(0), _ptr(out), _ptr(z), _ptr(m), ctypes.byref(written),
+         _stream(x))
+    if mask:
+        return out, z, (m if written.value else None)
     return out, z
 
 
@@ -584,13 +609,14 @@ class _RowMLP(torch.autograd.Function):
 
 
 def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, ws_tag: int = 0,
-                     prepared=None):
+                     prepared=None, mask=None):
     """The backward of mlp_rows(save=True) given dL/d(output) g_out [R, w_out]:
     dpac_mlp_rows_bwd (the input-gradient chain: G of every BN output, and dL/dx if
     want_x) then dpac_mlp_param_grads (if want_params).  params =
     DeepNN.trainable_variables(); prepared = mlp_prepare(..., want_wt=True) of the same
-    parameters if the caller already has it (one launch fewer); returns (g_x or None,
-    parameter gradients or None)."""
+    parameters if the caller already has it (one launch fewer); mask = the forward's sign
+    bits (mlp_rows(mask=True)) or None (z is read); returns (g_x or None, parameter
+    gradients or None)."""
     if prepared is None:
         L, gam, bet, Ws, b = _split_params(params)
         prepared = mlp_prepare(gam, bet, Ws, b, False, True)
@@ -598,8 +624,8 @@ def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, w
     R = x.shape[0]
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
     g_x = torch.empty(R, view.widths[0], dtype=x.dtype, device=x.device) if want_x else None
-    call("dpac_mlp_rows_bwd", _dtype_id(x), R, ctypes.byref(view.struct), _ptr_array(wt),
-         _ptr_array(wt_km), _ptr(z), _ptr(g_out.contiguous()), _ptr(G), _ptr(g_x), _stream(x))
+    call("dpac_mlp_rows_bwd_masked", _dtype_id(x), R, ctypes.byref(view.struct), _ptr_array(wt),
+         _ptr_array(wt_km), _ptr(z), _ptr(mask), _ptr(g_out.contiguous()), _ptr(G), _ptr(g_x), _stream(x))
     grads = mlp_param_grads(view, x, z, G, params, ws_tag) if want_params else None
     return g_x, grads
 
@@ -616,11 +642,12 @@ if CRITIC_TD1 not in ("fused", "split"):
 
 
 def mlp_rows_td1(eqp, view: MlpView, x: torch.Tensor, u: torch.Tensor, dw: torch.Tensor,
-                 save: bool = False):
+                 save: bool = False, mask: bool = False):
     """gdot [R] = Σ_j (σ(x,u)·dw)_j · G_j(x) for G = the network (width d in and out)
     over the rows x [R, d] (solver.py:179-184 without G ever written), one
     dpac_mlp_rows_fwd_td1 launch; u [R, c] and dw [R, d] row-aligned with x.  With
-    save=True also the backward saves z [R, Σ widths[1:]]."""
+    save=True also the backward saves z [R, Σ widths[1:]]; with mask=True (and save)
+    returns (gdot, z, sign-bit mask or None) as mlp_rows does."""
     _require_gpu(x, u, dw, *view.tensors)
     _check_same(x, u, dw, *view.tensors)
     if x.dim() != 2 or x.stride(1) != 1:
@@ -630,9 +657,13 @@ def mlp_rows_td1(eqp, view: MlpView, x: torch.Tensor, u: torch.Tensor, dw: torch
         raise ValueError("mlp_rows_td1: u [R, c] and dw [R, d] must be row-aligned with x")
     gdot = torch.empty(R, dtype=x.dtype, device=x.device)
     z = torch.empty(R, sum(view.widths[1:]), dtype=x.dtype, device=x.device) if save else None
-    call("dpac_mlp_rows_fwd_td1", ctypes.byref(eqp), _dtype_id(x), R, ctypes.byref(view.struct),
+    m = _row_mask_buffer(view, x) if (save and mask) else None
+    written = ctypes.c_int32(0)
+    call("dpac_mlp_rows_fwd_td1_masked", ctypes.byref(eqp), _dtype_id(x), R, ctypes.byref(view.struct),
          ctypes.c_void_p(x.data_ptr()), x.stride(0), _ptr(u.contiguous()), _ptr(dw.contiguous()),
-         _ptr(gdot), _ptr(z), _stream(x))
+         _ptr(gdot), _ptr(z), _ptr(m), ctypes.byref(written), _stream(x))
+    if mask:
+        return gdot, z, (m if written.value else None)
     return gdot, z
 
 
@@ -677,15 +708,16 @@ def td_assemble_bwd_gdot(eqp, dt, coef, g_y):
 
 
 def row_mlp_backward_td1(eqp, rs, params, x, z, u, dw, g_gdot, want_params: bool = True,
-                         ws_tag: int = 0):
+                         ws_tag: int = 0, mask=None):
     """row_mlp_backward for mlp_rows_td1: dpac_mlp_rows_bwd_td1 (dL/dG = g_gdot·σ dw in
-    its prologue) then dpac_mlp_param_grads; returns the parameter gradients."""
+    its prologue; mask: the forward's sign bits or None) then dpac_mlp_param_grads; returns
+    the parameter gradients."""
     L, gam, bet, Ws, b = _split_params(params)
     view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, False, True)
     R = x.shape[0]
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
-    call("dpac_mlp_rows_bwd_td1", ctypes.byref(eqp), _dtype_id(x), R, ctypes.byref(view.struct),
-         _ptr_array(wt), _ptr_array(wt_km), _ptr(z), ctypes.c_void_p(x.data_ptr()), x.stride(0),
+    call("dpac_mlp_rows_bwd_td1_masked", ctypes.byref(eqp), _dtype_id(x), R, ctypes.byref(view.struct),
+         _ptr_array(wt), _ptr_array(wt_km), _ptr(z), _ptr(mask), ctypes.c_void_p(x.data_ptr()), x.stride(0),
          _ptr(u.contiguous()), _ptr(dw.contiguous()), _ptr(g_gdot.contiguous()), _ptr(G), None,
          _stream(x))
     return mlp_param_grads(view, x, z, G, params, ws_tag) if want_params else None

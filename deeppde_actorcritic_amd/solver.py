@@ -688,11 +688,12 @@ class ActorCriticSolver(object):
             fused = ops.CRITIC_TD1 == "fused"
             if fused:  # G never written, only its TD1 dots
                 u_rows, dw_rows = u.reshape(N * B, -1), d.dw.reshape(N * B, -1)
-                gdot, zG = ops.mlp_rows_td1(eqp, Gnet.mlp_view(), rows, u_rows, dw_rows, save=True)
+                gdot, zG, mG = ops.mlp_rows_td1(eqp, Gnet.mlp_view(), rows, u_rows, dw_rows, save=True,
+                                                mask=ops.ROW_MASK)
                 y, disc = ops.td_assemble_gdot(eqp, x, u, dt, coef, gdot.view(N, B),
                                                cost_order=_lib.COST_CRITIC)
             else:
-                G, zG = ops.mlp_rows(Gnet.mlp_view(), rows, save=True)
+                G, zG, mG = ops.mlp_rows(Gnet.mlp_view(), rows, save=True, mask=ops.ROW_MASK)
                 y, disc = ops.td_assemble(eqp, mc.td, x, u, d.dw, dt, coef, G.view(N, B, -1),
                                           cost_order=_lib.COST_CRITIC)
             xv = torch.cat([x[0], x[N], d.x_bdry])
@@ -703,10 +704,10 @@ class ActorCriticSolver(object):
             g_out, neg_g = ops.critic_loss_grad(Vout, y, disc, self.bsde.Z_tf(d.x_bdry), 100.0 / B, DELTA_CLIP)
             if fused:
                 g_gdot = ops.td_assemble_bwd_gdot(eqp, dt, coef, neg_g)
-                back = (g_gdot.reshape(N * B), rows, zG, u_rows, dw_rows)
+                back = (g_gdot.reshape(N * B), rows, zG, mG, u_rows, dw_rows)
             else:
                 gG = ops.td_assemble_bwd(eqp, x, u, d.dw, dt, coef, neg_g)
-                back = (gG.reshape(N * B, -1), rows, zG)
+                back = (gG.reshape(N * B, -1), rows, zG, mG)
         return (xv, zV, g_out, prepV), back
 
     def critic_grads_v(self, vstate):
@@ -724,14 +725,14 @@ class ActorCriticSolver(object):
         dpac_mlp_param_grads, on their own scratch buffer: they run beside the BPTT)."""
         net = self.model_critic.NN_value_grad
         with torch.no_grad():
-            if len(front) == 6:  # fused TD1: dL/dG formed from dL/dgdot in the prologue
-                _, g_gdot, rows, z, u_rows, dw_rows = front
+            if len(front) == 7:  # fused TD1: dL/dG formed from dL/dgdot in the prologue
+                _, g_gdot, rows, z, m, u_rows, dw_rows = front
                 return ops.row_mlp_backward_td1(self.bsde.params(), net.bn_rs,
                                                 net.trainable_variables(), rows, z, u_rows,
-                                                dw_rows, g_gdot, True, ws_tag=1)
-            _, gG, rows, z = front
+                                                dw_rows, g_gdot, True, ws_tag=1, mask=m)
+            _, gG, rows, z, m = front
             _, grads = ops.row_mlp_backward(net.bn_rs, net.trainable_variables(), rows, z, gG,
-                                            False, True, ws_tag=1)
+                                            False, True, ws_tag=1, mask=m)
         return grads
 
     def train_iteration(self, data_critic, data_actor, total=None):

@@ -54,9 +54,10 @@ extern "C" {
  * images) and dpac_mlp_prepare writes them.  4: the split-fp16 images are fragment-major
  * (below) and the float fused rollout / BPTT (dpac_rollout_nn_fwd[_masked],
  * dpac_rollout_nn_bwd_masked) read them too.  5: adds dpac_critic_loss_grad.  6: dpac_mlp gains
- * `status` (the split-fp16 range guard, below).  Bindings must refuse a library of another
- * version. */
-#define DPAC_ABI_VERSION 6
+ * `status` (the split-fp16 range guard, below).  7: adds the row kernels' sign-bit mask
+ * (dpac_mlp_rows_mask_bytes, dpac_mlp_rows_{fwd,bwd}[_td1]_masked).  Bindings must refuse a
+ * library of another version. */
+#define DPAC_ABI_VERSION 7
 
 /* status codes besides hipError_t values */
 #define DPAC_OK 0
@@ -404,6 +405,38 @@ int dpac_mlp_rows_bwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows
                           const void* const* weight_t_km, const void* save_z, const void* x,
                           int64_t ldx, const void* u, const void* dw, const void* g_gdot,
                           void* G, void* g_x, void* stream);
+
+/* The row kernels with a sign-bit mask (round 5, ABI 7).  The backward chain needs of the
+ * forward's saved z only whether each hidden BN output was positive (the activation factor
+ * 1 + [y > 0], solver.py:269); the split-fp16 forward records those bits as it computes them,
+ * save_mask = dpac_mlp_rows_mask_bytes bytes laid out [Σ_h ceil(width[h] / 4)][rows] over the
+ * hidden layers h = 1..n_hidden in order: byte (q_h + q) * rows + r, q_h = Σ_{1<=k<h}
+ * ceil(width[k] / 4), holds at bit e (0..3) whether BN_h's output of row r, feature 4 q + e, is
+ * > 0 (bits past width[h] are 0).  The masked backward reads those bytes instead of z (z is
+ * still required: the parameter gradients and the exact-f32 fallback read it).  The mask is
+ * written only by the float split-fp16 forward (every weight_x3 given) and only with save_z:
+ * *mask_written (host, optional) reports whether it was; pass it to the backward only then.
+ * Results are bitwise those of the unmasked entry points (tests/test_gpu_mlp.py).
+ * dpac_mlp_rows_mask_bytes: the bytes for `rows` rows, 0 where no mask is written (float64,
+ * no split-fp16 images), -1 on a bad argument. */
+int64_t dpac_mlp_rows_mask_bytes(const dpac_mlp* net, int32_t dtype, int64_t rows);
+int dpac_mlp_rows_fwd_masked(int32_t dtype, int64_t rows, const dpac_mlp* net, const void* x,
+                             int64_t ldx, void* out, void* save_z, uint8_t* save_mask,
+                             int32_t* mask_written, void* stream);
+int dpac_mlp_rows_bwd_masked(int32_t dtype, int64_t rows, const dpac_mlp* net,
+                             const void* const* weight_t, const void* const* weight_t_km,
+                             const void* save_z, const uint8_t* save_mask, const void* g_out,
+                             void* G, void* g_x, void* stream);
+int dpac_mlp_rows_fwd_td1_masked(const dpac_eqn_params* eq, int32_t dtype, int64_t rows,
+                                 const dpac_mlp* net, const void* x, int64_t ldx, const void* u,
+                                 const void* dw, void* gdot, void* save_z, uint8_t* save_mask,
+                                 int32_t* mask_written, void* stream);
+int dpac_mlp_rows_bwd_td1_masked(const dpac_eqn_params* eq, int32_t dtype, int64_t rows,
+                                 const dpac_mlp* net, const void* const* weight_t,
+                                 const void* const* weight_t_km, const void* save_z,
+                                 const uint8_t* save_mask, const void* x, int64_t ldx,
+                                 const void* u, const void* dw, const void* g_gdot, void* G,
+                                 void* g_x, void* stream);
 
 /* ---- parameter gradients of a dpac_mlp over independent rows -------------
  * What GradientTape returns for DeepNN's trainable variables (solver.py:88,95

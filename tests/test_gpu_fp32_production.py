@@ -157,7 +157,8 @@ def test_fp32_production_gradients_vs_oracle_tape(name, B):
     assert min(dc[0].shape[0], da[0].shape[0]) > 1024  # still the 16-row fast path
     # critic: the production split step, on one batch
     front = sp.critic_front(dc)
-    assert len(front) == 6, "the fused TD1 critic path did not run"
+    assert len(front) == 7, "the fused TD1 critic path did not run"
+    assert front[4] is not None, "the G network's sign-bit mask was not written"
     gp_c = front[0] + sp.critic_G_back(front)
     go_c, _ = so.grad_critic(dc, False, False)
     # actor: forward with saves (sign-bit mask) + BPTT kernels
@@ -232,7 +233,7 @@ def test_fp32_full_size_shards_sum_to_whole_batch(name, total, world):
 
     def grads(data):
         front = sp.critic_front(data)
-        assert len(front) == 6  # fused TD1 critic
+        assert len(front) == 7  # fused TD1 critic
         gc = [g.detach().double() for g in front[0] + sp.critic_G_back(front)]
         ga = [g.detach().double() for g in sp.actor_grads_from(sp.actor_forward(data))]
         return gc + ga

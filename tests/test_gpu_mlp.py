@@ -360,6 +360,66 @@ def test_row_mlp_stacked_input_and_errors():
                                  None, None) == _lib.DPAC_EINVAL  # ldx < d
 
 
+@pytest.mark.parametrize("hidden,R", [((200, 200, 200), 20000), ((200, 200, 200), 777), ((52, 100, 36), 1234),
+                                      ((24, 40), 33)])
+@pytest.mark.parametrize("td1", [False, True])
+def test_row_backward_sign_mask_bitwise(hidden, R, td1, monkeypatch):
+    """Round 5: the split-fp16 row forward records the hidden BN outputs'
+    sign bits (dpac_mlp_rows_fwd[_td1]_masked) and the backward chain reads them instead of z
+    (dpac_mlp_rows_bwd[_td1]_masked).  The mask's bits equal [shift_h + z_h * scale_h > 0]
+    formed from the saved z (f32, the kernels' expression), and the masked backward's G,
+    dL/dx and parameter gradients equal the z-reading backward's bit for bit (ragged row
+    counts, widths that are not multiples of 4 or 16, the TD1 prologue)."""
+    monkeypatch.setattr(ops, "MLP_MATH", "x3")
+    cfg = full_config("LQR", 20, hidden=hidden, dtype="float32")
+    net = psol.DeepNN(cfg, "critic_grad", torch.Generator().manual_seed(R), torch.float32, DEV)
+    gen = torch.Generator(device=DEV).manual_seed(R + 7)
+    x = torch.randn(R, 20, generator=gen, device=DEV) * 0.5
+    params = [p.detach() for p in net.trainable_variables()]
+    prep = net.mlp_prepared()
+    view = prep[0]
+    if td1:
+        eqp = peq.LQR(cfg.eqn_config).params()
+        u = torch.randn(R, 20, generator=gen, device=DEV)
+        dw = torch.randn(R, 20, generator=gen, device=DEV)
+        g_gdot = torch.randn(R, generator=gen, device=DEV) / R
+        out, z, mask = ops.mlp_rows_td1(eqp, view, x, u, dw, save=True, mask=True)
+        out0, z0 = ops.mlp_rows_td1(eqp, view, x, u, dw, save=True)
+        res = {m: ops.row_mlp_backward_td1(eqp, net.bn_rs, params, x, z, u, dw, g_gdot, True, mask=m)
+               for m in (None, mask)}
+        chk = lambda a, b: [torch.equal(s, t) for s, t in zip(a, b)]
+    else:
+        g_out = torch.randn(R, 20, generator=gen, device=DEV) / R
+        out, z, mask = ops.mlp_rows(view, x, save=True, mask=True)
+        out0, z0 = ops.mlp_rows(view, x, save=True)
+        res = {m: ops.row_mlp_backward(net.bn_rs, params, x, z, g_out, True, True, prepared=prep, mask=m)
+               for m in (None, mask)}
+        chk = lambda a, b: [torch.equal(a[0], b[0])] + [torch.equal(s, t) for s, t in zip(a[1], b[1])]
+    torch.cuda.synchronize()
+    assert mask is not None and mask.dtype == torch.uint8
+    assert torch.equal(out, out0) and torch.equal(z, z0)  # writing the mask changes nothing else
+    # the bits against the saved z
+    widths = view.widths
+    nq = sum((w + 3) // 4 for w in widths[1:-1])
+    assert mask.numel() == nq * R
+    mk = mask.view(nq, R)
+    zo, qo = 0, 0
+    for h in range(1, len(widths) - 1):
+        w = widths[h]
+        y = view.shifts[h] + z[:, zo:zo + w] * view.scales[h]
+        pos = torch.zeros(R, (w + 3) // 4 * 4, dtype=torch.int32, device=DEV)
+        pos[:, :w] = (y > 0).int()
+        bits = (pos.view(R, -1, 4) << torch.arange(4, device=DEV, dtype=torch.int32)).sum(2)
+        assert torch.equal(mk[qo:qo + (w + 3) // 4].t().int(), bits), h
+        zo, qo = zo + w, qo + (w + 3) // 4
+    assert all(chk(res[mask], res[None]))
+    # the float64 path writes no mask
+    net64 = psol.DeepNN(full_config("LQR", 20, hidden=hidden), "critic_grad", torch.Generator().manual_seed(1),
+                        torch.float64, DEV)
+    _, _, m64 = ops.mlp_rows(net64.mlp_view(), x.double(), save=True, mask=True)
+    assert m64 is None
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_adam_kernel_matches_foreach_update(dtype):
     """dpac_adam_apply (one launch over a list of tensors, more than one launch's 32)

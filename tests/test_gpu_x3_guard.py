@@ -212,7 +212,7 @@ def test_fp32_production_gradients_with_out_of_range_networks_vs_oracle():
     dc = so.bsde.sample_normal(B, N)
     da = so.bsde.sample_normal(B, N)
     front = sp.critic_front(dc)
-    assert len(front) == 6
+    assert len(front) == 7
     gp_c = front[0] + sp.critic_G_back(front)
     go_c, _ = so.grad_critic(dc, False, False)
     fwd = sp.actor_forward(da)

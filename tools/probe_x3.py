@@ -57,9 +57,19 @@ def main():
         def bwd():
             _lib.call("dpac_mlp_rows_bwd", _lib.F32, R, ctypes.byref(bview.struct), ops._ptr_array(wt),
                       ops._ptr_array(wt_km), ops._ptr(z), ops._ptr(g), ops._ptr(G), None, ops._stream(x))
+        _, _, mask = ops.mlp_rows(view, x, save=True, mask=True)
+
+        def bwd_masked():
+            _lib.call("dpac_mlp_rows_bwd_masked", _lib.F32, R, ctypes.byref(bview.struct), ops._ptr_array(wt),
+                      ops._ptr_array(wt_km), ops._ptr(z), ops._ptr(mask), ops._ptr(g), ops._ptr(G), None,
+                      ops._stream(x))
         res = {"fwd_saves": timeit(lambda: ops.mlp_rows(view, x, save=True)),
+               "fwd_saves_mask": timeit(lambda: ops.mlp_rows(view, x, save=True, mask=True)),
                "fwd_td1_saves": timeit(lambda: ops.mlp_rows_td1(eqp, view, x, u, dw, save=True)),
+               "fwd_td1_saves_mask": timeit(lambda: ops.mlp_rows_td1(eqp, view, x, u, dw, save=True, mask=True)),
                "bwd_chain": timeit(bwd)}
+        if mask is not None:
+            res["bwd_chain_masked"] = timeit(bwd_masked)
         if "--pg" in sys.argv:  # the parameter gradients (every layer + the chunk reduce)
             bwd()
             res["param_grads"] = timeit(lambda: ops.mlp_param_grads(view, x, z, G, params))
