@@ -185,6 +185,12 @@ inline bool pgx_w_ok(const PgArgs<float>& a, int l) {
   return K > 32 && H > 32 && K <= 208 && K % 4 == 0 && a.zoff[l] % 4 == 0 && out;
 }
 
+// DPAC_PG_MERGE=0: every layer its own launch (timing comparisons; bitwise the same results)
+inline bool pg_merge() {
+  const char* e = getenv("DPAC_PG_MERGE");  // read per launch
+  return !(e && e[0] == '0');
+}
+
 template <int NTI, bool L0 = false>
 int pgw_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   using PL = PgwPlan<NTI, L0>;
@@ -242,6 +248,13 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
         a.status = net.status;
         const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
         for (int l = 0; l <= a.L; ++l) {
+          // two adjacent wide layers of the 13-tile bin: one launch (k_param_grads_x3w, lsel < 0)
+          if (pg_merge() && l >= 1 && l + 1 <= a.L && pgx_w_ok(a, l) && pgx_w_ok(a, l + 1) &&
+              (a.width[l] + 15) / 16 > 8 && (a.width[l + 1] + 15) / 16 > 8) {
+            if (int e = pgw_launch<13>(a, -l, (nch + 7) / 8 * 16, s0)) return e;
+            ++l;
+            continue;
+          }
           // layers the split kernel does not cover (a wide layer with more than 13 input
           // tiles; an input layer wider than 32 or into a layer of <= 32) take the f32
           // kernel on the same chunks and partial layout
@@ -362,10 +375,7 @@ X3Args x3_args(const dpac_mlp& net, int64_t rows, const void* const* img, const 
   a.bias = m.bias;
   a.ztot = m.ztot;
   a.gtot = m.gtot;
-  for (int h = 1, q = 0; h <= a.L + 1; ++h) {  // the sign-bit bytes' quad rows per hidden layer
-    a.mqoff[h] = q;
-    if (h <= a.L) q += (a.width[h] + 3) / 4;
-  }
+  a.nblk = (rows + 63) / 64;  // the sign-bit mask's 64-row blocks
   if (td) {
     a.td_x = (const float*)td->x;
     a.td_ldx = td->ldx;
@@ -416,7 +426,7 @@ int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void
       xa.out = (float*)out;
       xa.z = (float*)save_z;
       xa.status = net.status;
-      xa.mask = save_z ? mask : nullptr;
+      xa.mask = (save_z && kX3RT == 4) ? reinterpret_cast<uint32_t*>(mask) : nullptr;  // 64-row blocks
       if (int e = x3_launch(k_mlp_rows_fwd_x3, xa, s)) return e;
       if (written && xa.mask) *written = 1;
       if (!net.status) return 0;
@@ -442,7 +452,7 @@ int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const voi
       a.G = (float*)G;
       a.g_x = (float*)g_x;
       a.status = net.status;
-      a.mask = const_cast<uint8_t*>(mask);
+      a.mask = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(mask));
       if (int e = mask ? x3_launch(k_mlp_rows_bwd_x3<true>, a, s, kX3RowsB, kX3LdsBytesB)
                        : x3_launch(k_mlp_rows_bwd_x3<false>, a, s, kX3RowsB, kX3LdsBytesB))
         return e;
@@ -493,10 +503,9 @@ int mlp_rows_bwd_launch(int dtype, int64_t rows, const dpac_mlp& net, const void
 }
 
 int64_t mlp_rows_mask_bytes(int dtype, int64_t rows, const dpac_mlp& net) {
-  if (dtype != DPAC_F32 || !x3_all(net, net.weight_x3)) return 0;  // only the split-fp16 forward writes it
-  int64_t q = 0;
-  for (int h = 1; h <= net.n_hidden; ++h) q += (net.width[h] + 3) / 4;
-  return q * rows;
+  // only the split-fp16 forward writes it, over 64-row workgroups (dpac_mlp_x3.h X3Args::mask)
+  if (dtype != DPAC_F32 || !x3_all(net, net.weight_x3) || kX3RT != 4) return 0;
+  return (int64_t)net.n_hidden * ((rows + 63) / 64) * kX3MaskWords * 4;
 }
 
 int64_t mlp_param_grads_ws_bytes(int dtype, int64_t rows, const dpac_mlp& net) {

@@ -258,6 +258,7 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
   for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) bad |= epi.store(j, rt, ah[rt][j] + al[rt][j] * kX3LoInv, wave, lane);
+  epi.finish(lane);
   return bad;
 }
 
@@ -279,6 +280,7 @@ __device__ __forceinline__ bool x3_layer(const _Float16* in, int K, int Nout, co
   } else if (mine == 2) {
     return x3_layer_t<2, 0, RT>(in, K, Nout, Wx3, wave, lane, epi);
   }
+  epi.finish(lane);  // a wave without tiles: its (zero) sign-bit mask word
   return false;
 }
 
@@ -307,12 +309,18 @@ struct X3Args {
   float* gdot;
   const float* g_gdot;
   uint32_t* status;  // the range guard (dpac_mlp.status), or null
-  // the hidden activations' sign bits (dpac.h dpac_mlp_rows_fwd_masked): byte (mqoff[h] + q) *
-  // rows + r holds bit e = [BN_h(z_h)[r][4 q + e] > 0]; written by the forward, read by the
-  // backward instead of z (null: not written / z read)
-  uint8_t* mask;
-  int mqoff[DPAC_MLP_MAX_HIDDEN + 2];
+  // the hidden activations' sign bits (dpac.h dpac_mlp_rows_fwd_masked): per hidden layer h
+  // (1..L) and 64-row block b, 512 words; word ((h - 1) nblk + b) 512 + 64 w + 16 q + r holds at
+  // bit 4 (2 rt + j) + e whether BN_h's output of row 64 b + 16 rt + r, feature 16 (w + 8 j) +
+  // 4 q + e, is > 0 — exactly the nibbles lane 16 q + r of wave w holds in the 64-row forward
+  // (x3_f0), so each lane writes one word per layer.  Written by the forward, read by the
+  // backward instead of z (null: not written / z read).
+  uint32_t* mask;
+  int64_t nblk;  // ceil(rows / 64)
 };
+constexpr int kX3MaskWords = 512;  // per hidden layer and 64-row block
+static_assert(4 % kX3RTB == 0, "a backward workgroup's row tiles lie in one 64-row mask block");
+static_assert(kX3Waves == 8 && kX3MaxNT == 2, "the mask word holds 2 tiles x 4 row tiles of one lane");
 
 // the lane's feature quad f0 = 16 tile + 4 (l >> 4) and how many of its features exist
 __device__ __forceinline__ int x3_f0(int wave, int j, int lane) { return (wave + kX3Waves * j) * 16 + 4 * (lane >> 4); }
@@ -333,8 +341,8 @@ struct X3FwdEpi {
   int z_ld;                  // floats
   __amdgpu_buffer_rsrc_t ro; // out: the workgroup's rows
   float *zp, *op;            // the same rows as plain pointers (x3_store4's partial quads)
-  uint8_t* mp;               // hidden: the layer's sign-bit bytes at the workgroup's first row, or null
-  int64_t mld;               // bytes between a quad's rows and the next quad's (= rows)
+  uint32_t* mp;              // hidden: the layer's mask words of the workgroup's 64-row block, or null
+  uint32_t mword;            // the lane's sign nibbles, bit 4 (2 rt + j) + e
   x3f4 s[kX3MaxNT], sh[kX3MaxNT], bb[kX3MaxNT];
   template <int NT>
   __device__ __forceinline__ void pre(int wave, int lane) {
@@ -352,6 +360,9 @@ struct X3FwdEpi {
   }
   template <int NT>
   __device__ __forceinline__ void post(int, int) {}
+  __device__ __forceinline__ void finish(int lane) {  // one mask word per lane and layer
+    if (MODE == kX3Hidden && mp) mp[lane] = mword;
+  }
   __device__ __forceinline__ bool store(int j, int rt, x3f4 zv, int wave, int lane) {
     const int f0 = x3_f0(wave, j, lane), nv = x3_nvalid(f0, Nout);
     const int row = rt * 16 + (lane & 15);
@@ -366,7 +377,7 @@ struct X3FwdEpi {
         nib |= (e < nv && y[e] > 0.f) ? 1u << e : 0u;
         y[e] = e < nv ? y[e] + fmaxf(y[e], 0.f) : 0.f;  // y + relu(y) (solver.py:269)
       }
-      if (mp && row < rows_live && nv > 0) mp[(int64_t)(f0 >> 2) * mld + row] = (uint8_t)nib;
+      if (row < rows_live) mword |= nib << (4 * (2 * rt + j));
       return x3_put4(img, row, f0, y);
     } else if (MODE == kX3Stage) {
 #pragma unroll
@@ -399,12 +410,12 @@ struct X3BwdEpi {
   const float* rinv;           // LDS: 2^-e of each row (undoes the chain's row scale)
   const float* zp;             // plain pointers to the same rows (partial quads)
   float *gp, *xp;
-  const uint8_t* mp;           // MASKED: layer l's sign-bit bytes at the workgroup's first row
-  int64_t mld;                 // MASKED: bytes between quads (= rows)
+  const uint32_t* mp;          // MASKED: layer l's mask words of the workgroup's 64-row block
+  int mshift;                  // MASKED: 4 * 2 * (the workgroup's first row tile within the block)
   x3f4 s[kX3MaxNT], sh[kX3MaxNT];
   float ri[RT];
   x3f4 zz[MASKED ? 1 : kX3MaxNT][MASKED ? 1 : RT];  // z_l of the lane's quads, loaded in post()
-  uint32_t mb[MASKED ? kX3MaxNT : 1][MASKED ? RT : 1];  // MASKED: their sign nibbles
+  uint32_t mword;              // MASKED: the lane's mask word (loaded in post())
   template <int NT>
   __device__ __forceinline__ void pre(int wave, int lane) {
 #pragma unroll
@@ -423,15 +434,7 @@ struct X3BwdEpi {
   template <int NT>
   __device__ __forceinline__ void post(int wave, int lane) {  // every z load, then one wait
     if constexpr (!FIRST && MASKED) {
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int f0 = x3_f0(wave, j, lane), nv = x3_nvalid(f0, Nout);
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          const int row = rt * 16 + (lane & 15);
-          mb[j][rt] = (nv > 0 && row < rows_live) ? (uint32_t)mp[(int64_t)(f0 >> 2) * mld + row] : 0u;
-        }
-      }
+      mword = mp[lane] >> mshift;
     } else if constexpr (!FIRST) {
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
@@ -443,12 +446,13 @@ struct X3BwdEpi {
       }
     }
   }
+  __device__ __forceinline__ void finish(int) {}
   __device__ __forceinline__ bool store(int j, int rt, x3f4 v, int wave, int lane) {
     const int f0 = x3_f0(wave, j, lane), nv = x3_nvalid(f0, Nout);
     const int row = rt * 16 + (lane & 15);
     if constexpr (!FIRST && MASKED) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = v[e] * (((mb[j][rt] >> e) & 1u) ? 2.f : 1.f);  // d(y + relu(y))/dy
+      for (int e = 0; e < 4; ++e) v[e] = v[e] * (((mword >> (4 * (2 * rt + j) + e)) & 1u) ? 2.f : 1.f);  // d(y + relu(y))/dy
     } else if constexpr (!FIRST) {
       const x3f4 y = sh[j] + zz[j][rt] * s[j];  // the forward's BN_l output
 #pragma unroll
@@ -534,17 +538,19 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
     if (l < a.L) {
       X3FwdEpi<kX3Hidden> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], nullptr, rows_live, Nout, img(pq ^ 1),
                               nullptr, rz, a.z != nullptr, a.ztot, make_rsrc(nullptr, 0), zp, nullptr,
-                              a.mask ? a.mask + (int64_t)a.mqoff[l + 1] * a.rows + row0 : nullptr, a.rows};
+                              a.mask ? a.mask + ((int64_t)l * a.nblk + blockIdx.x) * kX3MaskWords + wave * 64
+                                     : nullptr,
+                              0u};
       bad |= x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     } else if (a.gdot) {
       X3FwdEpi<kX3Stage> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], a.bias, rows_live, Nout, nullptr,
                              reinterpret_cast<float*>(img(pq ^ 1)), rz, a.z != nullptr, a.ztot, make_rsrc(nullptr, 0),
-                             zp, nullptr, nullptr, 0};
+                             zp, nullptr, nullptr, 0u};
       x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     } else {
       X3FwdEpi<kX3Out> epi{2 + 2 * l, a.scale[l + 1], a.shift[l + 1], a.bias, rows_live, Nout, nullptr, nullptr,
                            rz, a.z != nullptr, a.ztot, x3_rows_rsrc(a.out, row0, rows_live, Nout), zp,
-                           a.out + row0 * Nout, nullptr, 0};
+                           a.out + row0 * Nout, nullptr, 0u};
       x3_layer(img(pq), a.width[l], Nout, a.wx3[l], wave, lane, epi);
     }
     __syncthreads();
@@ -618,7 +624,9 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
                                   x3_rows_rsrc(MASKED ? nullptr : a.z + a.zoff[l], row0, rows_live, a.ztot), a.ztot,
                                   rg, a.gtot, make_rsrc(nullptr, 0), false, nullptr, rinv,
                                   a.z + a.zoff[l] + row0 * a.ztot, gp, nullptr,
-                                  MASKED ? a.mask + (int64_t)a.mqoff[l] * a.rows + row0 : nullptr, a.rows};
+                                  MASKED ? a.mask + ((int64_t)(l - 1) * a.nblk + (row0 >> 6)) * kX3MaskWords + wave * 64
+                                         : nullptr,
+                                  8 * (int)((row0 & 63) >> 4)};
       bad |= x3_layer<kX3RTB>(img(pq), a.width[l + 1], a.width[l], a.wx3[l], wave, lane, epi);
     } else {
       X3BwdEpi<true> epi{2 + 2 * L, nullptr, nullptr, rows_live, a.width[0], img(pq ^ 1), make_rsrc(nullptr, 0), 0, rg, a.gtot,

@@ -82,19 +82,82 @@ __device__ __forceinline__ nxf4 nx_mma(nxh8 a, nxh8 b, nxf4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-// four consecutive features f0..f0+3 (f0 % 4 == 0) of one row, split, as two 8-byte LDS writes;
-// true if one of them is outside the split range (dpac.h dpac_mlp.status)
-__device__ __forceinline__ bool nx_put4(_Float16* img, int ld, int row, int f0, nxf4 v) {
-  nxh4 h, l;
+#ifndef DPAC_NX_FOLD
+#define DPAC_NX_FOLD 1  // the narrow product after the last wide layer folded into its epilogue (round 5)
+#endif
+
+// four values split into hi / lo halves; true if one of them is outside the split range
+// (dpac.h dpac_mlp.status)
+__device__ __forceinline__ bool nx_split4(nxf4 v, nxh4& h, nxh4& l) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     h[e] = (_Float16)v[e];
     l[e] = (_Float16)((v[e] - (float)h[e]) * kNxLo);
   }
+  return x3_bad4(v[0], v[1], v[2], v[3]);
+}
+
+// four consecutive features f0..f0+3 (f0 % 4 == 0) of one row, split, as two 8-byte LDS writes;
+// true if one of them is outside the split range (dpac.h dpac_mlp.status)
+__device__ __forceinline__ bool nx_put4(_Float16* img, int ld, int row, int f0, nxf4 v) {
+  nxh4 h, l;
+  const bool bad = nx_split4(v, h, l);
   _Float16* p = img + row * ld + (f0 >> 5) * 64 + (f0 & 31);
   *reinterpret_cast<nxh4*>(p) = h;
   *reinterpret_cast<nxh4*>(p + 32) = l;
-  return x3_bad4(v[0], v[1], v[2], v[3]);
+  return bad;
+}
+
+// The narrow product that follows the last 13-tile layer (the forward's output layer, the
+// BPTT's gradient into a_0), folded into that layer's epilogue (round 5): wave w already holds,
+// for row l & 15, the features 16 w + 4 q + e (its tile w) and 16 (w + 8) + 4 q + e (tile w + 8),
+// q = l >> 4, e = 0..3 — exactly the 8 k of a B fragment if the wave's 32-k "chunk" is those 32
+// features in that order.  So each wave multiplies its own activations, straight from registers,
+// by the matching rows of the weight: A fragments (output column l & 15 of output tile t, the
+// same permuted k) gathered once per launch from the fragment-major image W (Nout columns over
+// nch 32-k chunks; rows past the layer and missing chunks read 0).  Wave w's partial of output
+// tile t goes to the split-K partial slot w: no LDS image of the last layer, no barrier before
+// the narrow product.
+__device__ __forceinline__ void nx_fold_w(nxh8 (&fh)[2], nxh8 (&fl)[2], const _Float16* W, int Nout, int nch,
+                                          int wave, int lane) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const int ntiles = (Nout + 15) / 16;
+  const __amdgpu_buffer_rsrc_t r = make_rsrc(W, (uint32_t)(ntiles * nch * 2048));
+  const int q = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+      const int tile = wave + 8 * sd;              // the 16-feature tile of the layer's k
+      const int c = tile >> 1;                     // its 32-k chunk in the image
+      const int qq = 2 * (tile & 1) + (q >> 1);    // the image lane group holding k = 16 tile + 4 q ..
+      const uint32_t off = (t < ntiles && c < nch)
+                               ? (uint32_t)((t * nch + c) * 2048 + (qq * 16 + (lane & 15)) * 16 + 8 * (q & 1))
+                               : kOOB;
+      const nxh4 h = __builtin_bit_cast(nxh4, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+      const nxh4 l = __builtin_bit_cast(nxh4, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(off + 1024u), 0, 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        fh[t][4 * sd + e] = h[e];
+        fl[t][4 * sd + e] = l[e];
+      }
+    }
+  }
+}
+
+// the folded narrow product of a wave's split activations (bh, bl: the permuted B fragment) into
+// its split-K partial slot (kNxPartLd floats per row, output tile t at column 16 t)
+__device__ __forceinline__ void nx_fold_prod(const nxh8 (&fh)[2], const nxh8 (&fl)[2], nxh8 bh, nxh8 bl,
+                                             float* part, int wave, int lane) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    nxf4 a[3] = {nxf4{0.f, 0.f, 0.f, 0.f}, nxf4{0.f, 0.f, 0.f, 0.f}, nxf4{0.f, 0.f, 0.f, 0.f}};
+    a[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[t], bh, a[0], 0, 0, 0);
+    a[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[t], bl, a[1], 0, 0, 0);
+    a[2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[t], bh, a[2], 0, 0, 0);
+    *reinterpret_cast<nxf4*>(part + (wave * 16 + (lane & 15)) * kNxPartLd + 16 * t + 4 * (lane >> 4)) =
+        a[0] + (a[1] + a[2]) * kNxLoInv;
+  }
 }
 
 __device__ __forceinline__ bool nx_put1(_Float16* img, int ld, int row, int col, float v) {
@@ -220,12 +283,16 @@ __device__ __forceinline__ int nx_mask_idx(int lane) {  // byte of the tile this
 // y + relu(y) split into the next image, the mask byte.  bn: LDS [scale | shift] of layer h,
 // zero past Nout.  Tiles past the layer are skipped (wave-uniform).  Returns whether a split
 // operand left the range.
-template <bool SAVE, bool MASK>
+// FOLD: the last hidden layer: instead of the next image, its activations multiply the folded
+// output weights (fh, fl; nx_fold_w) into the wave's split-K partial slot of `part`.
+template <bool SAVE, bool MASK, bool FOLD = false>
 __device__ __forceinline__ bool nx_fwd_epi(const nxf4 (&acc)[2][3], int wave, int lane, int Nout, const float* bn,
                                            _Float16* out, float* zrow0, int ztot, bool zvec, int rows_live,
-                                           uint8_t* mtile, bool mrow) {
+                                           uint8_t* mtile, bool mrow, const nxh8 (*fh)[2] = nullptr,
+                                           const nxh8 (*fl)[2] = nullptr, float* part = nullptr) {
   const int row = lane & 15;
   bool bad = false;
+  nxh8 bh = nxh8{0, 0, 0, 0, 0, 0, 0, 0}, bl = bh;  // FOLD: the wave's permuted B fragment
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int tl = wave + 8 * j;
@@ -252,23 +319,39 @@ __device__ __forceinline__ bool nx_fwd_epi(const nxf4 (&acc)[2][3], int wave, in
       nib |= (e < nv && y[e] > 0.f) ? 1u << e : 0u;
       y[e] = e < nv ? y[e] + fmaxf(y[e], 0.f) : 0.f;  // y + relu(y) (solver.py:269)
     }
-    bad |= nx_put4(out, kNxLd, row, f0, y);
+    if constexpr (FOLD) {
+      nxh4 h, l;
+      bad |= nx_split4(y, h, l);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bh[4 * j + e] = h[e];
+        bl[4 * j + e] = l[e];
+      }
+    } else {
+      bad |= nx_put4(out, kNxLd, row, f0, y);
+    }
     if constexpr (MASK && !(DPAC_NX_ABLATE & 2)) {
       const uint32_t w = nx_quad_gather(nib, lane);
       if (mrow) mtile[64 * tl + nx_mask_idx(lane)] = (uint8_t)nx_pick4(w, lane & 3);
     }
   }
+  if constexpr (FOLD) nx_fold_prod(*fh, *fl, bh, bl, part, wave, lane);
   return bad;
 }
 
 // BPTT epilogue of hidden layer h: the activation factor 1 + [y_h > 0] from the forward's
 // mask bytes, G_h = v * 2^(e-1) (the row's scale undone) to global, v split into the next image.
 // Returns whether a split operand left the range.
+// FOLD: hidden layer 1: instead of the next image, the (scaled) gradient multiplies the folded
+// weights of the product into a_0's gradient (fh, fl; nx_fold_w) into the wave's partial slot.
+template <bool FOLD = false>
 __device__ __forceinline__ bool nx_bwd_epi(const nxf4 (&acc)[2][3], int wave, int lane, int Nout,
                                            const uint32_t (&mb)[2], _Float16* out, float* grow0, int gtot,
-                                           bool gvec, int rows_live, float ri) {
+                                           bool gvec, int rows_live, float ri, const nxh8 (*fh)[2] = nullptr,
+                                           const nxh8 (*fl)[2] = nullptr, float* part = nullptr) {
   const int row = lane & 15, i = lane & 3;
   bool bad = false;
+  nxh8 bh = nxh8{0, 0, 0, 0, 0, 0, 0, 0}, bl = bh;  // FOLD: the wave's permuted B fragment
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int tl = wave + 8 * j;
@@ -290,8 +373,19 @@ __device__ __forceinline__ bool nx_bwd_epi(const nxf4 (&acc)[2][3], int wave, in
           if (e < nv) gp[e] = gv[e];
       }
     }
-    bad |= nx_put4(out, kNxLd, row, f0, v);
+    if constexpr (FOLD) {
+      nxh4 h, l;
+      bad |= nx_split4(v, h, l);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bh[4 * j + e] = h[e];
+        bl[4 * j + e] = l[e];
+      }
+    } else {
+      bad |= nx_put4(out, kNxLd, row, f0, v);
+    }
   }
+  if constexpr (FOLD) nx_fold_prod(*fh, *fl, bh, bl, part, wave, lane);
   return bad;
 }
 
@@ -368,6 +462,8 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
   const __amdgpu_buffer_rsrc_t rs_u = make_rsrc(a.u, a.u ? slab_u * (uint32_t)a.N : 0u);
   const int L = mlp.L, c_out = mlp.width[L + 1];
   const int nch_out = (mlp.width[L] + 31) / 32;  // split-K: wave w < nch_out multiplies chunk w
+  constexpr bool kFold = DPAC_NX_FOLD != 0;
+  const int nparts = kFold ? kNnWaves : nch_out;  // split-K partials the step lanes add
   int zalign = mlp.ztot;  // 16-byte z saves where every hidden block starts 4-aligned
   for (int h = 1; h <= L; ++h) zalign |= mlp.zoff[h];
   const bool zvec = (zalign & 3) == 0;
@@ -401,7 +497,10 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
   // weights: the narrow products' for the whole launch, the first wide layer's
   nxh8 rih[1][2], ril[1][2], roh[1][2], rol[1][2], wh[kNxRing][2], wl[kNxRing][2];
   nx_loadw<1>(rih, ril, mlp.wx3[0], mlp.width[1], 1, 0, wave, wave + 8, lane);
-  nx_loadw<1>(roh, rol, mlp.wx3[L], c_out, nch_out, wave, 0, 1, lane);
+  if constexpr (kFold)
+    nx_fold_w(roh[0], rol[0], mlp.wx3[L], c_out, nch_out, wave, lane);  // the output layer, folded
+  else
+    nx_loadw<1>(roh, rol, mlp.wx3[L], c_out, nch_out, wave, 0, 1, lane);
   if (L >= 2) nx_loadw<kNxRing>(wh, wl, mlp.wx3[1], mlp.width[2], kNxWide, 0, wave, wave + 8, lane);
 
   auto write_a0 = [&](const T (&xv)[M]) {  // addcmul(beta0, x, gamma0/sqrt(1+eps)), solver.py:265
@@ -429,9 +528,14 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
     {  // hidden layer 1 from a0 (narrow K, resident weights)
       nxf4 acc[2][3];
       nx_prod<1, kNxLd0, 0>(in0, 0, rih, ril, acc, lane);
-      bad |= nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[1], s_bn, img(0),
-                             SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[1] : nullptr, mlp.ztot, zvec, rows_live,
-                             mt, mrow);
+      if (kFold && L == 1)
+        bad |= nx_fwd_epi<SAVE, MASK, kFold>(acc, wave, lane, mlp.width[1], s_bn, img(0),
+                                             SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[1] : nullptr, mlp.ztot,
+                                             zvec, rows_live, mt, mrow, &roh[0], &rol[0], part);
+      else
+        bad |= nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[1], s_bn, img(0),
+                                      SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[1] : nullptr, mlp.ztot, zvec,
+                                      rows_live, mt, mrow);
     }
     NN_MARK(t, 1);
     __syncthreads();
@@ -446,24 +550,32 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
 #endif
       const int ln = l + 1 < L ? l + 1 : 1;  // the next wide layer (this step's or the next one's first)
       nx_loadw<kNxRing>(wh, wl, mlp.wx3[ln], mlp.width[ln + 1], kNxWide, 0, wave, wave + 8, lane);
-      bad |= nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[l + 1], s_bn + l * kNxBnLd, img(l),
-                             SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[l + 1] : nullptr, mlp.ztot, zvec,
-                             rows_live, MASK ? mt + 13 * 64 * l : nullptr, mrow);
+      if (kFold && l + 1 == L)  // the last hidden layer: the output layer in its epilogue
+        bad |= nx_fwd_epi<SAVE, MASK, kFold>(acc, wave, lane, mlp.width[l + 1], s_bn + l * kNxBnLd, img(l),
+                                             SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[l + 1] : nullptr,
+                                             mlp.ztot, zvec, rows_live, MASK ? mt + 13 * 64 * l : nullptr, mrow,
+                                             &roh[0], &rol[0], part);
+      else
+        bad |= nx_fwd_epi<SAVE, MASK>(acc, wave, lane, mlp.width[l + 1], s_bn + l * kNxBnLd, img(l),
+                                      SAVE ? a.save_z + rowt * mlp.ztot + mlp.zoff[l + 1] : nullptr, mlp.ztot,
+                                      zvec, rows_live, MASK ? mt + 13 * 64 * l : nullptr, mrow);
       NN_MARK(t, 1 + 2 * l);
       __syncthreads();
       NN_MARK(t, 2 + 2 * l);
     }
-    if (wave < nch_out) {  // output layer: chunk `wave` of hidden layer L for both output tiles
-      nxf4 acc[2][3];
-      nx_prod<1, kNxLd, 0>(img(L - 1), wave, roh, rol, acc, lane);
+    if (!kFold) {
+      if (wave < nch_out) {  // output layer: chunk `wave` of hidden layer L for both output tiles
+        nxf4 acc[2][3];
+        nx_prod<1, kNxLd, 0>(img(L - 1), wave, roh, rol, acc, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        *reinterpret_cast<nxf4*>(part + (wave * 16 + (lane & 15)) * kNxPartLd + 16 * j + 4 * (lane >> 4)) =
-            nx_sum(acc[j]);
+        for (int j = 0; j < 2; ++j)
+          *reinterpret_cast<nxf4*>(part + (wave * 16 + (lane & 15)) * kNxPartLd + 16 * j + 4 * (lane >> 4)) =
+              nx_sum(acc[j]);
+      }
+      NN_MARK(t, 1 + 2 * L);
+      __syncthreads();
+      NN_MARK(t, 2 + 2 * L);
     }
-    NN_MARK(t, 1 + 2 * L);
-    __syncthreads();
-    NN_MARK(t, 2 + 2 * L);
     if (!stepper) return;
     // ---- u_t from the partials (fixed wave order), then the transition (step lanes) ----
     const float* pr = part + g * kNxPartLd;
@@ -473,7 +585,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
     for (int m = 0; m < MC; ++m) {
       const int j = ownu.valid(m) ? ownu.j(m) : 0;
       T z = pr[j];
-      for (int w = 1; w < nch_out; ++w) z += pr[w * 16 * kNxPartLd + j];
+      for (int w = 1; w < nparts; ++w) z += pr[w * 16 * kNxPartLd + j];
       if (SAVE && live && ownu.valid(m)) zrow[j] = z;
       T yv = z + oB[m];     // addmm(b, y, W) (solver.py:270)
       yv = yv * oS[m];
@@ -481,7 +593,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_x3(const E eq, const 
     }
     if (mlp.ekn) {  // y[:, :d] / (1e-15 + relu(y[:, d]) + |y[:, :d]|) (solver.py:272-274)
       T zc = pr[CD];
-      for (int w = 1; w < nch_out; ++w) zc += pr[w * 16 * kNxPartLd + CD];
+      for (int w = 1; w < nparts; ++w) zc += pr[w * 16 * kNxPartLd + CD];
       if (SAVE && live && lc.p == 0) zrow[CD] = zc;
       T yc = zc + eB;
       yc = eSh + yc * eS;
@@ -567,6 +679,8 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
   const Own<CD, P> ownu(lc.p);
   const int L = mlp.L;
   const int nch0 = (mlp.width[1] + 31) / 32;  // split-K of the product into a_0's gradient
+  constexpr bool kFold = DPAC_NX_FOLD != 0;
+  const int nparts = kFold ? kNnWaves : nch0;  // split-K partials the step lanes add
   int galign = a.gtot;  // 16-byte G stores where every hidden block starts 4-aligned
   for (int h = 1; h <= L; ++h) galign |= a.goff[h];
   const bool gvec = (galign & 3) == 0;
@@ -595,7 +709,10 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
   // weights of the transposed chain (weight_t_x3[i]: [width[i]][ceil(width[i+1] / 32)][64])
   nxh8 rih[1][2], ril[1][2], roh[1][2], rol[1][2], wh[kNxRing][2], wl[kNxRing][2];
   nx_loadw<1>(rih, ril, a.wtx3[L], mlp.width[L], 1, 0, wave, wave + 8, lane);
-  nx_loadw<1>(roh, rol, a.wtx3[0], mlp.width[0], nch0, wave, 0, 1, lane);
+  if constexpr (kFold)
+    nx_fold_w(roh[0], rol[0], a.wtx3[0], mlp.width[0], nch0, wave, lane);  // a_0's gradient, folded
+  else
+    nx_loadw<1>(roh, rol, a.wtx3[0], mlp.width[0], nch0, wave, 0, 1, lane);
   if (L >= 2) nx_loadw<kNxRing>(wh, wl, a.wtx3[L - 1], mlp.width[L - 1], kNxWide, 0, wave, wave + 8, lane);
   if (a.g_xN && stepper) own.load_masked(a.g_xN + lc.b * D, lam);
   T gD = (a.g_disc && stepper) ? a.g_disc[lc.b] : T(0);
@@ -698,8 +815,13 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
     {  // hidden layer L from the output's gradient (narrow K, resident weights)
       nxf4 acc[2][3];
       nx_prod<1, kNxLd0, 0>(in0, 0, rih, ril, acc, lane);
-      bad |= nx_bwd_epi(acc, wave, lane, mlp.width[L], mb[L - 1], img(0), a.G + (rowt + row0) * a.gtot + a.goff[L],
-                        a.gtot, gvec, rows_live, ri);
+      if (kFold && L == 1)
+        bad |= nx_bwd_epi<kFold>(acc, wave, lane, mlp.width[L], mb[L - 1], img(0),
+                                 a.G + (rowt + row0) * a.gtot + a.goff[L], a.gtot, gvec, rows_live, ri, &roh[0],
+                                 &rol[0], part);
+      else
+        bad |= nx_bwd_epi(acc, wave, lane, mlp.width[L], mb[L - 1], img(0), a.G + (rowt + row0) * a.gtot + a.goff[L],
+                          a.gtot, gvec, rows_live, ri);
     }
     NN_MARK(t, 3);
     __syncthreads();
@@ -714,23 +836,30 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
 #endif
       const int ln = l - 1 >= 1 ? l - 1 : L - 1;  // the next wide layer (this step's or the next one's first)
       nx_loadw<kNxRing>(wh, wl, a.wtx3[ln], mlp.width[ln], kNxWide, 0, wave, wave + 8, lane);
-      bad |= nx_bwd_epi(acc, wave, lane, mlp.width[l], mb[l - 1], img(L - l), a.G + (rowt + row0) * a.gtot + a.goff[l],
-                        a.gtot, gvec, rows_live, ri);
+      if (kFold && l == 1)  // hidden layer 1: the product into a_0's gradient in its epilogue
+        bad |= nx_bwd_epi<kFold>(acc, wave, lane, mlp.width[l], mb[l - 1], img(L - l),
+                                 a.G + (rowt + row0) * a.gtot + a.goff[l], a.gtot, gvec, rows_live, ri, &roh[0],
+                                 &rol[0], part);
+      else
+        bad |= nx_bwd_epi(acc, wave, lane, mlp.width[l], mb[l - 1], img(L - l),
+                          a.G + (rowt + row0) * a.gtot + a.goff[l], a.gtot, gvec, rows_live, ri);
       NN_MARK(t, 3 + 2 * (L - l));
       __syncthreads();
       NN_MARK(t, 4 + 2 * (L - l));
     }
-    if (wave < nch0) {  // dL/d a_0: chunk `wave` of hidden layer 1's gradient for both tiles
-      nxf4 acc[2][3];
-      nx_prod<1, kNxLd, 0>(img(L - 1), wave, roh, rol, acc, lane);
+    if (!kFold) {
+      if (wave < nch0) {  // dL/d a_0: chunk `wave` of hidden layer 1's gradient for both tiles
+        nxf4 acc[2][3];
+        nx_prod<1, kNxLd, 0>(img(L - 1), wave, roh, rol, acc, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        *reinterpret_cast<nxf4*>(part + (wave * 16 + (lane & 15)) * kNxPartLd + 16 * j + 4 * (lane >> 4)) =
-            nx_sum(acc[j]);
+        for (int j = 0; j < 2; ++j)
+          *reinterpret_cast<nxf4*>(part + (wave * 16 + (lane & 15)) * kNxPartLd + 16 * j + 4 * (lane >> 4)) =
+              nx_sum(acc[j]);
+      }
+      NN_MARK(t, 3 + 2 * L);
+      __syncthreads();
+      NN_MARK(t, 4 + 2 * L);
     }
-    NN_MARK(t, 3 + 2 * L);
-    __syncthreads();
-    NN_MARK(t, 4 + 2 * L);
     if (stepper) {  // G_0 and dL/dx_t = direct part + G_0 * s_0 (a_0 = beta_0 + x * s_0)
       const float* pr = part + g * kNxPartLd;
       const T rg = s_rinv[g];
@@ -739,7 +868,7 @@ __global__ __launch_bounds__(kNnThreads) void k_rollout_nn_bwd_x3(const E eq, co
       for (int m = 0; m < M; ++m) {
         const int j = own.valid(m) ? own.j(m) : 0;
         T v = pr[j];
-        for (int w = 1; w < nch0; ++w) v += pr[w * 16 * kNxPartLd + j];
+        for (int w = 1; w < nparts; ++w) v += pr[w * 16 * kNxPartLd + j];
         v = v * rg;
         if (live && own.valid(m)) g0[j] = v;
         lam[m] = gxd[m] + (own.valid(m) ? v * s0[m] : T(0));

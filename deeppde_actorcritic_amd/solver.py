@@ -688,12 +688,14 @@ class ActorCriticSolver(object):
             fused = ops.CRITIC_TD1 == "fused"
             if fused:  # G never written, only its TD1 dots
                 u_rows, dw_rows = u.reshape(N * B, -1), d.dw.reshape(N * B, -1)
-                gdot, zG, mG = ops.mlp_rows_td1(eqp, Gnet.mlp_view(), rows, u_rows, dw_rows, save=True,
-                                                mask=ops.ROW_MASK)
+                gdot, zG, *mG = ops.mlp_rows_td1(eqp, Gnet.mlp_view(), rows, u_rows, dw_rows, save=True,
+                                                 mask=ops.ROW_MASK)
+                mG = mG[0] if mG else None  # the sign-bit mask, or None (DPAC_ROW_MASK=0, float64)
                 y, disc = ops.td_assemble_gdot(eqp, x, u, dt, coef, gdot.view(N, B),
                                                cost_order=_lib.COST_CRITIC)
             else:
-                G, zG, mG = ops.mlp_rows(Gnet.mlp_view(), rows, save=True, mask=ops.ROW_MASK)
+                G, zG, *mG = ops.mlp_rows(Gnet.mlp_view(), rows, save=True, mask=ops.ROW_MASK)
+                mG = mG[0] if mG else None
                 y, disc = ops.td_assemble(eqp, mc.td, x, u, d.dw, dt, coef, G.view(N, B, -1),
                                           cost_order=_lib.COST_CRITIC)
             xv = torch.cat([x[0], x[N], d.x_bdry])

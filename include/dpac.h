@@ -409,10 +409,12 @@ int dpac_mlp_rows_bwd_td1(const dpac_eqn_params* eq, int32_t dtype, int64_t rows
 /* The row kernels with a sign-bit mask (round 5, ABI 7).  The backward chain needs of the
  * forward's saved z only whether each hidden BN output was positive (the activation factor
  * 1 + [y > 0], solver.py:269); the split-fp16 forward records those bits as it computes them,
- * save_mask = dpac_mlp_rows_mask_bytes bytes laid out [Σ_h ceil(width[h] / 4)][rows] over the
- * hidden layers h = 1..n_hidden in order: byte (q_h + q) * rows + r, q_h = Σ_{1<=k<h}
- * ceil(width[k] / 4), holds at bit e (0..3) whether BN_h's output of row r, feature 4 q + e, is
- * > 0 (bits past width[h] are 0).  The masked backward reads those bytes instead of z (z is
+ * save_mask = dpac_mlp_rows_mask_bytes bytes of 32-bit words: per hidden layer h = 1..n_hidden
+ * and 64-row block b (nblk = ceil(rows / 64) of them), 512 words; word
+ * ((h - 1) nblk + b) * 512 + 64 w + 16 q + r (w < 8, q < 4, r < 16) holds at bit 4 (2 t + j) + e
+ * (t, e < 4; j < 2) whether BN_h's output of row 64 b + 16 t + r, feature 16 (w + 8 j) + 4 q + e,
+ * is > 0 (0 past width[h] and past the last row) — the split-fp16 kernels' accumulator layout,
+ * so each lane writes and reads one word per layer.  The masked backward reads them instead of z (z is
  * still required: the parameter gradients and the exact-f32 fallback read it).  The mask is
  * written only by the float split-fp16 forward (every weight_x3 given) and only with save_z:
  * *mask_written (host, optional) reports whether it was; pass it to the backward only then.

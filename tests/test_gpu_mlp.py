@@ -154,7 +154,13 @@ def test_param_grads_merged_group_kernel_bitwise(widths, R, gscale, monkeypatch)
     like = scales + shifts + Ws + [b]
     monkeypatch.delenv("DPAC_PG_X3", raising=False)
     monkeypatch.delenv("DPAC_PGX_W", raising=False)
+    monkeypatch.delenv("DPAC_PG_MERGE", raising=False)
     merged = ops.mlp_param_grads(view, x, z, G, like)
+    monkeypatch.setenv("DPAC_PG_MERGE", "0")  # round 5: adjacent wide layers in one launch, or not
+    single = ops.mlp_param_grads(view, x, z, G, like)
+    monkeypatch.delenv("DPAC_PG_MERGE")
+    for a, c in zip(merged, single):
+        assert torch.equal(a, c), float((a - c).abs().max())
     monkeypatch.setenv("DPAC_PGX_W", "0")
     two = ops.mlp_param_grads(view, x, z, G, like)
     monkeypatch.setenv("DPAC_PG_X3", "0")
@@ -398,20 +404,25 @@ def test_row_backward_sign_mask_bitwise(hidden, R, td1, monkeypatch):
     torch.cuda.synchronize()
     assert mask is not None and mask.dtype == torch.uint8
     assert torch.equal(out, out0) and torch.equal(z, z0)  # writing the mask changes nothing else
-    # the bits against the saved z
+    # the bits against the saved z (dpac.h: word ((h-1) nblk + b) 512 + 64 w + 16 q + r, bit
+    # 4 (2 t + j) + e = [BN_h output of row 64 b + 16 t + r, feature 16 (w + 8 j) + 4 q + e > 0])
     widths = view.widths
-    nq = sum((w + 3) // 4 for w in widths[1:-1])
-    assert mask.numel() == nq * R
-    mk = mask.view(nq, R)
-    zo, qo = 0, 0
-    for h in range(1, len(widths) - 1):
+    L = len(widths) - 2
+    nblk = (R + 63) // 64
+    assert mask.numel() == L * nblk * 512 * 4
+    words = mask.view(torch.int32).view(L, nblk, 8, 4, 16).long() & 0xFFFFFFFF
+    shift = (4 * (2 * torch.arange(4, device=DEV).view(4, 1, 1) + torch.arange(2, device=DEV).view(1, 2, 1))
+             + torch.arange(4, device=DEV).view(1, 1, 4))  # [t, j, e]
+    zo = 0
+    for h in range(1, L + 1):
         w = widths[h]
         y = view.shifts[h] + z[:, zo:zo + w] * view.scales[h]
-        pos = torch.zeros(R, (w + 3) // 4 * 4, dtype=torch.int32, device=DEV)
-        pos[:, :w] = (y > 0).int()
-        bits = (pos.view(R, -1, 4) << torch.arange(4, device=DEV, dtype=torch.int32)).sum(2)
-        assert torch.equal(mk[qo:qo + (w + 3) // 4].t().int(), bits), h
-        zo, qo = zo + w, qo + (w + 3) // 4
+        pos = torch.zeros(nblk * 64, 256, dtype=torch.int64, device=DEV)
+        pos[:R, :w] = (y > 0).long()
+        pos = pos.view(nblk, 4, 16, 2, 8, 4, 4).permute(0, 4, 5, 2, 1, 3, 6)  # [b, w, q, r, t, j, e]
+        expect = (pos << shift).sum((4, 5, 6))
+        assert torch.equal(words[h - 1], expect), h
+        zo += w
     assert all(chk(res[mask], res[None]))
     # the float64 path writes no mask
     net64 = psol.DeepNN(full_config("LQR", 20, hidden=hidden), "critic_grad", torch.Generator().manual_seed(1),
