@@ -185,6 +185,18 @@ inline bool pgx_w_ok(const PgArgs<float>& a, int l) {
   return K > 32 && H > 32 && K <= 208 && K % 4 == 0 && a.zoff[l] % 4 == 0 && out;
 }
 
+// Layer l >= 1 on the merged-group kernel's 13-tile bin: a wide hidden layer (pgx_w_ok), or the
+// output layer of <= 32 columns (one launch with the wide layers before it; its 16 waves then
+// hold 2 column tiles, the others idle) — both with 129..208 inputs.
+inline bool pgw13_ok(const PgArgs<float>& a, int l) {
+  const int K = a.width[l], H = a.width[l + 1];
+  if (K <= 128 || K > 208 || K % 4 != 0 || a.zoff[l] % 4 != 0) return false;
+  if (pgx_w_ok(a, l)) return true;
+  return l == a.L && H <= 32 && H % 4 == 0 && a.ztot % 4 == 0 && a.zoff[l + 1] % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(a.z) & 15) == 0 && (getenv("DPAC_PG_MERGE_OUT") == nullptr ||
+                                                          getenv("DPAC_PG_MERGE_OUT")[0] != '0');
+}
+
 // DPAC_PG_MERGE=0: every layer its own launch (timing comparisons; bitwise the same results)
 inline bool pg_merge() {
   const char* e = getenv("DPAC_PG_MERGE");  // read per launch
@@ -248,11 +260,13 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
         a.status = net.status;
         const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
         for (int l = 0; l <= a.L; ++l) {
-          // two adjacent wide layers of the 13-tile bin: one launch (k_param_grads_x3w, lsel < 0)
-          if (pg_merge() && l >= 1 && l + 1 <= a.L && pgx_w_ok(a, l) && pgx_w_ok(a, l + 1) &&
-              (a.width[l] + 15) / 16 > 8 && (a.width[l + 1] + 15) / 16 > 8) {
-            if (int e = pgw_launch<13>(a, -l, (nch + 7) / 8 * 16, s0)) return e;
-            ++l;
+          // a run of adjacent layers of the merged-group kernel's 13-tile bin (the wide hidden
+          // layers, and the output layer after them): one launch (k_param_grads_x3w, lsel < 0)
+          int nl = 0;
+          while (pg_merge() && l >= 1 && l + nl <= a.L && pgw13_ok(a, l + nl)) ++nl;
+          if (nl >= 2) {
+            if (int e = pgw_launch<13>(a, -(l + 8 * nl), (nch + 7) / 8 * 8 * nl, s0)) return e;
+            l += nl - 1;
             continue;
           }
           // layers the split kernel does not cover (a wide layer with more than 13 input

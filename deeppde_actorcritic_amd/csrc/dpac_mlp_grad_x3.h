@@ -459,11 +459,12 @@ __device__ __forceinline__ void pgw_row_dma(const float* src, uint32_t voff, uns
                : "=&s"(keep) : "v"(voff), "s"(m0), "s"(base) : "memory");
 }
 
-// lsel >= 0: layer lsel, chunk blockIdx.x.  lsel < 0 (round 5, L0 = false): layers -lsel and
-// -lsel + 1 in ONE launch, XCD-aware: each group of 16 workgroups holds 8 chunks x the 2 layers,
-// and a chunk's two workgroups are 8 apart (the dispatcher deals workgroups round-robin over the
-// 8 XCDs, so they share an XCD and run together): z_{l+1}, layer l's BN operand and layer l+1's
-// A, is read by both at about the same time and the second read can hit L2 / the Infinity Cache.
+// lsel >= 0: layer lsel, chunk blockIdx.x.  lsel < 0 (round 5, L0 = false): -lsel = l0 + 8 nl,
+// layers l0 .. l0 + nl - 1 in ONE launch, XCD-aware: each group of 8 nl workgroups holds 8 chunks
+// x the nl layers, and a chunk's workgroups are 8 apart (the dispatcher deals workgroups
+// round-robin over the 8 XCDs, so they share an XCD and run together): z_{l+1}, layer l's BN
+// operand and layer l+1's A, is read by both at about the same time and the second read can hit
+// L2 / the Infinity Cache.
 template <int NTI, bool L0 = false>
 __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<float> a, const int lsel) {
   using PL = PgwPlan<NTI, L0>;
@@ -479,8 +480,9 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   int* const s_cexp = reinterpret_cast<int*>(s_cfac + CW);
   if (x3_status_set(a.status)) return;  // fell back: the f32 kernel after this one does the work
   const int64_t bx = blockIdx.x;
-  const int l = lsel >= 0 ? lsel : -lsel + (int)((bx >> 3) & 1);
-  const int64_t chunk = lsel >= 0 ? bx : (bx >> 4) * 8 + (bx & 7);
+  const int nl = lsel >= 0 ? 1 : (-lsel) >> 3;
+  const int l = lsel >= 0 ? lsel : ((-lsel) & 7) + (int)((bx >> 3) % nl);
+  const int64_t chunk = lsel >= 0 ? bx : (bx / (8 * nl)) * 8 + (bx & 7);
   if (chunk * a.rows_per_chunk >= a.rows) return;  // past the last chunk (merged grid), before any barrier
   bool bad = false;
   const int K = a.width[l], H = a.width[l + 1];
