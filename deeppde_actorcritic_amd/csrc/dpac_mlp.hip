@@ -197,20 +197,28 @@ inline bool pgw13_ok(const PgArgs<float>& a, int l) {
                                                           getenv("DPAC_PG_MERGE_OUT")[0] != '0');
 }
 
+static_assert(PgwPlan<13>::kSmem + kPgwRawG0c <= 160 * 1024, "a merged launch from the input layer fits the LDS");
+
 // DPAC_PG_MERGE=0: every layer its own launch (timing comparisons; bitwise the same results)
 inline bool pg_merge() {
   const char* e = getenv("DPAC_PG_MERGE");  // read per launch
   return !(e && e[0] == '0');
 }
+// DPAC_PG_MERGE_IN=0: the input layer keeps its own launch
+inline bool pg_merge_in() {
+  const char* e = getenv("DPAC_PG_MERGE_IN");  // read per launch
+  return pg_merge() && !(e && e[0] == '0');
+}
 
 template <int NTI, bool L0 = false>
-int pgw_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
+int pgw_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s, int extra_lds = 0) {
   using PL = PgwPlan<NTI, L0>;
   auto k = k_param_grads_x3w<NTI, L0>;
+  const int lds = PL::kSmem + extra_lds;  // + the merged input layer's compact G_0 slots
   if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, PL::kSmem))
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds))
     return (int)e;
-  hipLaunchKernelGGL(k, dim3((unsigned)nch), dim3(kPgwThreads), PL::kSmem, s, a, l);
+  hipLaunchKernelGGL(k, dim3((unsigned)nch), dim3(kPgwThreads), lds, s, a, l);
   return (int)hipGetLastError();
 }
 
@@ -262,10 +270,12 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
         for (int l = 0; l <= a.L; ++l) {
           // a run of adjacent layers of the merged-group kernel's 13-tile bin (the wide hidden
           // layers, and the output layer after them): one launch (k_param_grads_x3w, lsel < 0)
-          int nl = 0;
-          while (pg_merge() && l >= 1 && l + nl <= a.L && pgw13_ok(a, l + nl)) ++nl;
+          // (and the input layer before them, run by the same kernel at run time)
+          const bool in = l == 0 && pg_merge_in() && pgx_w_ok(a, 0);
+          int nl = in ? 1 : 0;
+          while (pg_merge() && (l >= 1 || in) && l + nl <= a.L && pgw13_ok(a, l + nl)) ++nl;
           if (nl >= 2) {
-            if (int e = pgw_launch<13>(a, -(l + 8 * nl), (nch + 7) / 8 * 8 * nl, s0)) return e;
+            if (int e = pgw_launch<13>(a, -(l + 8 * nl), (nch + 7) / 8 * 8 * nl, s0, in ? kPgwRawG0c : 0)) return e;
             l += nl - 1;
             continue;
           }

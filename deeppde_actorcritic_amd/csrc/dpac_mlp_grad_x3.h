@@ -431,7 +431,7 @@ struct PgwPlan {
   static constexpr int kRawG0 = kRawZ + kRaw;                 // L0: G_0 rows (the BN_0 sums)
   static constexpr int kCol = kRawG0 + (L0 ? kRaw : 0);       // s_cmax [4][256], s_cfac, s_cexp
   static constexpr int kSmem = kCol + (4 * kPgwCW + 2 * kPgwCW) * 4;
-  static_assert(4 * 2 * kPgwCW * 4 + (L0 ? 4 * 2 * KP * 4 : 0) <= kRawA, "BN sums' reduction fits the image bytes");
+  static_assert(4 * 2 * kPgwCW * 4 + 4 * 2 * KP * 4 <= kRawA, "BN sums' reduction fits the image bytes");
   static_assert(kSmem <= 160 * 1024, "LDS");
 };
 
@@ -459,12 +459,22 @@ __device__ __forceinline__ void pgw_row_dma(const float* src, uint32_t voff, uns
                : "=&s"(keep) : "v"(voff), "s"(m0), "s"(base) : "memory");
 }
 
+// The same copy of a row of at most 128 bytes into a compact 128-byte slot: only the lanes
+// inside the row (and lane 0) issue, so nothing lands past dst + 128.
+__device__ __forceinline__ void pgw_row_dma_128(const float* src, uint32_t bytes, int lane, unsigned char* dst) {
+  if ((uint32_t)lane * 16u < bytes || lane == 0) pgw_row_dma(src, (uint32_t)lane * 16u, dst);
+}
+constexpr int kPgwRawG0c = kPgxSR * 128;  // merged launches: G_0 rows in compact 128-byte slots (K <= 32)
+
 // lsel >= 0: layer lsel, chunk blockIdx.x.  lsel < 0 (round 5, L0 = false): -lsel = l0 + 8 nl,
 // layers l0 .. l0 + nl - 1 in ONE launch, XCD-aware: each group of 8 nl workgroups holds 8 chunks
 // x the nl layers, and a chunk's workgroups are 8 apart (the dispatcher deals workgroups
 // round-robin over the 8 XCDs, so they share an XCD and run together): z_{l+1}, layer l's BN
 // operand and layer l+1's A, is read by both at about the same time and the second read can hit
-// L2 / the Infinity Cache.
+// L2 / the Infinity Cache.  A merged launch may start at the input layer (l0 = 0, K <= 32): its
+// workgroups run the L0 variant's arithmetic at run time (BN_0 only, BN_0's sums from G_0 rows,
+// which land in compact slots after the plan's LDS: the launch adds kPgwRawG0c bytes), bitwise
+// k_param_grads_x3w<NTI, true>'s results.
 template <int NTI, bool L0 = false>
 __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<float> a, const int lsel) {
   using PL = PgwPlan<NTI, L0>;
@@ -493,8 +503,12 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   const int64_t r_begin = chunk * a.rows_per_chunk;
   const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
   const bool last = l == a.L;
-  const float* srcA = L0 ? a.x : a.z + a.zoff[l];  // L0: the network input (l = 0)
-  const int64_t ldA = L0 ? a.ldx : a.ztot;
+  const bool rt0 = !L0 && l == 0;   // the input layer inside a merged launch (see above)
+  const bool in0 = L0 || rt0;
+  const float* srcA = in0 ? a.x : a.z + a.zoff[l];  // L0: the network input (l = 0)
+  const int64_t ldA = in0 ? a.ldx : a.ztot;
+  const float* const rawG0 = reinterpret_cast<const float*>(smem + (L0 ? PL::kRawG0 : PL::kSmem));
+  const int g0ld = L0 ? CW : 32;  // floats per G_0 slot
   const float* gB = a.G + a.goff[l + 1];
   const float* zB = a.z + a.zoff[l + 1];
   const int64_t ld = a.ztot;
@@ -521,6 +535,7 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
       pgw_row_dma(srcA + row * ldA, voffA, smem + PL::kRawA + i * CW * 4);
       pgw_row_dma(zB + row * ld, voffZ, smem + PL::kRawZ + i * CW * 4);
       if constexpr (L0) pgw_row_dma(a.G + a.goff[0] + row * a.gtot, voffA, smem + PL::kRawG0 + i * CW * 4);
+      else if (rt0) pgw_row_dma_128(a.G + a.goff[0] + row * a.gtot, (uint32_t)K * 4u, lane, smem + PL::kSmem + i * 128);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -545,10 +560,10 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
         for (int i = 0; i < 8; ++i) {
           const float xv = rawA[(8 * rb + i) * CW + fl];
           const float y = ha + xv * sa;
-          if constexpr (L0) {  // BN_0 only (solver.py:260-262); its sums over the chunk's rows
+          if (in0) {  // BN_0 only (solver.py:260-262); its sums over the chunk's rows
             v[i] = fa ? y : 0.f;
             if (fa && r0 + 8 * rb + i < r_end) {
-              const float g0 = reinterpret_cast<const float*>(smem + PL::kRawG0)[(8 * rb + i) * CW + fl];
+              const float g0 = rawG0[(8 * rb + i) * g0ld + fl];
               cs0_b += g0;
               cs0_s += g0 * xv;
             }
@@ -646,12 +661,12 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   red[(rb * 2 + 0) * CW + fl] = csb_b;
   red[(rb * 2 + 1) * CW + fl] = csb_s;
   float* red0 = red + 4 * 2 * CW;  // L0: [4 rb][2][KP]
-  if (L0 && fl < KP) {
+  if (in0 && fl < KP) {
     red0[(rb * 2 + 0) * KP + fl] = cs0_b;
     red0[(rb * 2 + 1) * KP + fl] = cs0_s;
   }
   __syncthreads();
-  if (L0 && tid < K) {
+  if (in0 && tid < K) {
     float sb = 0.f, ss = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {

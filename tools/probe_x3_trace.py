@@ -41,16 +41,20 @@ def main():
     cfg = full_config("LQR", 20, hidden=(200, 200, 200), dtype="float32")
     net = psol.DeepNN(cfg, "critic_grad", torch.Generator().manual_seed(0), torch.float32, "cuda")
     x = torch.randn(R, 20, device="cuda") * 0.5
+    u = torch.randn(R, 20, device="cuda") * 0.5
+    dw = torch.randn(R, 20, device="cuda")
     g = torch.randn(R, 20, device="cuda") * 1e-3
+    from deeppde_actorcritic_amd import equation as peq
+    eqp = peq.LQR(cfg.eqn_config).params()
     ops.MLP_MATH = "x3"
     view = net.mlp_view()
-    for _ in range(3):
-        _, z = ops.mlp_rows(view, x, save=True)
+    for _ in range(3):  # the production forward of the critic's G network: TD1 dot fused, saves, mask
+        _, z, m = ops.mlp_rows_td1(eqp, view, x, u, dw, save=True, mask=True)
     torch.cuda.synchronize()
-    print(json.dumps({"fwd": table(lib, 10)}), flush=True)
+    print(json.dumps({"fwd_td1": table(lib, 10)}), flush=True)
     params = [p.detach() for p in net.trainable_variables()]
     for _ in range(3):
-        ops.row_mlp_backward(net.bn_rs, params, x, z, g, False, False)
+        ops.row_mlp_backward(net.bn_rs, params, x, z, g, False, False, mask=m)
     torch.cuda.synchronize()
     print(json.dumps({"bwd": table(lib, 10)}), flush=True)
 
