@@ -107,9 +107,9 @@ class Equation(object):
 
     # ---- device sampler (rocRAND Philox, keyed by global trajectory index) -----
     def sample_device(self, kind: str, num_sample: int, N: int, seed: int, traj_offset: int = 0,
-                      dtype=None) -> TrajectoryBatch:
+                      dtype=None, out=None) -> TrajectoryBatch:
         x0, dw, xb = ops.sample(self.params(), SAMPLE_TYPES[kind], num_sample, N, seed,
-                                traj_offset, dtype or torch_dtype(), _device())
+                                traj_offset, dtype or torch_dtype(), _device(), out=out)
         return TrajectoryBatch(x0, dw, xb)
 
     @staticmethod

@@ -59,16 +59,24 @@ def _check_same(ref: torch.Tensor, *others):
 
 # ---------------------------------------------------------------------------
 def sample(eqp, sample_type: int, num_sample: int, num_steps: int, seed: int,
-           traj_offset: int = 0, dtype=torch.float32, device=None, want_dw=True):
-    """On-device Philox sampler (equation.py:13-44 semantics, different stream)."""
+           traj_offset: int = 0, dtype=torch.float32, device=None, want_dw=True, out=None):
+    """On-device Philox sampler (equation.py:13-44 semantics, different stream).  out: existing
+    (x0 [B,d], dw [N,B,d], x_bdry [B,d]) buffers to draw into (contiguous, the call's dtype)."""
     device = torch.device(device if device is not None else "cuda")
     if device.type != "cuda":
         raise _lib.DpacUnavailable("dpac_sample needs a GPU device")
     _lib.load()
     d = eqp.dim
-    x0 = torch.empty(num_sample, d, dtype=dtype, device=device)
-    x_bdry = torch.empty(num_sample, d, dtype=dtype, device=device)
-    dw = torch.empty(num_steps, num_sample, d, dtype=dtype, device=device) if want_dw else None
+    if out is not None:
+        x0, dw, x_bdry = out
+        shapes = ((num_sample, d), (num_steps, num_sample, d), (num_sample, d))
+        for t, shp in zip((x0, dw, x_bdry), shapes):
+            if tuple(t.shape) != shp or t.dtype != dtype or not t.is_contiguous() or t.device != device:
+                raise ValueError(f"sample(out=): expected contiguous {dtype} {shp} on {device}")
+    else:
+        x0 = torch.empty(num_sample, d, dtype=dtype, device=device)
+        x_bdry = torch.empty(num_sample, d, dtype=dtype, device=device)
+        dw = torch.empty(num_steps, num_sample, d, dtype=dtype, device=device) if want_dw else None
     call("dpac_sample", ctypes.byref(eqp), sample_type, _DT[dtype], num_sample, num_steps,
          seed & 0xFFFFFFFFFFFFFFFF, traj_offset, _ptr(x0), _ptr(dw), _ptr(x_bdry), _stream(x0))
     return x0, dw, x_bdry

@@ -367,7 +367,8 @@ class _SplitActorGraphs:
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
             for dst, src in zip(self.static, batch):
-                dst.copy_(src)
+                if dst.data_ptr() != src.data_ptr():  # drawn in place by prefetch_samples: no copy
+                    dst.copy_(src)
             self.g_fwd.replay()
 
     def grads(self):
@@ -407,7 +408,8 @@ class _SplitCriticGraphs:
     def head(self, batch: TrajectoryBatch):
         """The head graph on the current stream."""
         for dst, src in zip(self.static, batch):
-            dst.copy_(src)
+            if dst.data_ptr() != src.data_ptr():  # drawn in place by prefetch_samples: no copy
+                dst.copy_(src)
         self.g_head.replay()
 
     def grads_v(self):
@@ -423,6 +425,13 @@ class _SplitCriticGraphs:
             self.g_back.replay()
         return list(self.back_out)
 
+
+# DPAC_GRAPH_SETS=2 (default): train_iteration alternates two sets of the split graphs and
+# prefetch_samples draws the next iteration's samples into the idle set's static inputs (no
+# copies in front of the graphs); 1: one set, the samples copied in (round 4's path).
+GRAPH_SETS = int(os.environ.get("DPAC_GRAPH_SETS", "2"))
+if GRAPH_SETS not in (1, 2):
+    raise ValueError(f"DPAC_GRAPH_SETS must be 1 or 2, got {GRAPH_SETS}")
 
 # DPAC_GBACK=late (default): the critic's G backward is launched on its side stream after V's
 # update and the actor's BPTT are queued, so it runs beside the BPTT and the actor's
@@ -517,6 +526,11 @@ class ActorCriticSolver(object):
         self._graphs = {}
         self._side = None
         self._side_g = None
+        # the split actor / critic graphs, two sets per shape used alternately (round 5): the
+        # next iteration's samples are drawn straight into the idle set's static inputs
+        self._gsets = {}          # (B, N_critic, N_actor) -> [(actor graphs, critic graphs)] * 2
+        self._parity = 0          # the set the next train_iteration uses
+        self._set_done = [None, None]  # event after the last iteration that used each set
 
     # ---- variables ---------------------------------------------------------
     def critic_variables(self):
@@ -526,7 +540,9 @@ class ActorCriticSolver(object):
         return self.model_actor.NN_control.trainable_variables()
 
     # ---- sampling (this rank's shard of every batch) -------------------------
-    def sample(self, num_sample, N, kind=None):
+    def sample(self, num_sample, N, kind=None, out=None):
+        """This rank's shard of a fresh batch; out (device sampler only): a TrajectoryBatch to
+        draw into (the same numbers)."""
         kind = kind or self.sample_type
         off, cnt = self.par.shard(num_sample)
         if self.sampler == "host":
@@ -536,7 +552,7 @@ class ActorCriticSolver(object):
             return Equation.to_native((x0[off:off + cnt], dw[off:off + cnt], xb[off:off + cnt]), self.dtype)
         self._calls += 1
         key = (self.seed * 0x9E3779B1 + self._calls) & 0xFFFFFFFFFFFFFFFF
-        return self.bsde.sample_device(kind, cnt, N, key, off, self.dtype)
+        return self.bsde.sample_device(kind, cnt, N, key, off, self.dtype, out=out)
 
     def sample_iteration(self, num_sample, N_critic, N_actor):
         """The (critic, actor) samples of one training iteration (solver.py:67-70): the pair
@@ -562,8 +578,20 @@ class ActorCriticSolver(object):
             return
         if self._sample_side is None:
             self._sample_side = torch.cuda.Stream()
-        with torch.cuda.stream(self._sample_side):  # fresh buffers: nothing to wait for
-            dc, da = self.sample(num_sample, N_critic), self.sample(num_sample, N_actor)
+        # the next iteration's graph set (train_iteration alternates two): its static inputs are
+        # drawn into in place, once the iteration that last read them is done, so the next
+        # iteration copies nothing in (round 5); otherwise fresh buffers
+        gset = self._gsets.get((num_sample, N_critic, N_actor)) if GRAPH_SETS == 2 else None
+        gset = gset[self._parity] if gset else None
+        with torch.cuda.stream(self._sample_side):
+            if gset is not None:
+                sg, cg = gset
+                if self._set_done[self._parity] is not None:
+                    torch.cuda.current_stream().wait_event(self._set_done[self._parity])
+                dc = self.sample(num_sample, N_critic, out=cg.static)
+                da = self.sample(num_sample, N_actor, out=sg.static)
+            else:  # fresh buffers: nothing to wait for
+                dc, da = self.sample(num_sample, N_critic), self.sample(num_sample, N_actor)
             ready = torch.cuda.Event()
             ready.record()
         self._next_samples = ((num_sample, N_critic, N_actor), dc, da, ready)
@@ -750,26 +778,30 @@ class ActorCriticSolver(object):
             self.train_step_actor(data_actor, total)
             return
         da = Equation.to_native(data_actor, self.dtype)
-        key = ("actor_split", tuple(da.dw.shape))
-        sg = self._graphs.get(key)
-        if sg is None:
-            if self._side is None:
-                self._side = torch.cuda.Stream()
-            sg = self._graphs[key] = _SplitActorGraphs(self.actor_forward, self.actor_grads_from,
-                                                       da, self._side)
-        sg.launch_forward(da)
+        if self._side is None:
+            self._side = torch.cuda.Stream()
         if not self._critic_split_ok():
+            key = ("actor_split", tuple(da.dw.shape))
+            sg = self._graphs.get(key)
+            if sg is None:
+                sg = self._graphs[key] = _SplitActorGraphs(self.actor_forward, self.actor_grads_from,
+                                                           da, self._side)
+            sg.launch_forward(da)
             self.train_step_critic(data_critic, total)
             cg = None
         else:
             dc = Equation.to_native(data_critic, self.dtype)
-            ckey = ("critic_split", tuple(dc.dw.shape))
-            cg = self._graphs.get(ckey)
-            if cg is None:
-                if self._side_g is None:
-                    self._side_g = torch.cuda.Stream()
-                cg = self._graphs[ckey] = _SplitCriticGraphs(self.critic_head, self.critic_grads_v,
-                                                             self.critic_G_back, dc, self._side_g)
+            if self._side_g is None:
+                self._side_g = torch.cuda.Stream()
+            spec = (dc.x0.shape[0] * self.par.world if total is None else total, dc.dw.shape[0], da.dw.shape[0])
+            sets = self._gsets.setdefault(spec, [None, None])
+            p = self._parity
+            if sets[p] is None:
+                sets[p] = (_SplitActorGraphs(self.actor_forward, self.actor_grads_from, da, self._side),
+                           _SplitCriticGraphs(self.critic_head, self.critic_grads_v, self.critic_G_back, dc,
+                                              self._side_g))
+            sg, cg = sets[p]
+            sg.launch_forward(da)
             ccnt = dc.x0.shape[0]
             ctot = total or ccnt * self.par.world
             cg.head(dc)
@@ -795,6 +827,10 @@ class ActorCriticSolver(object):
         g, gG = self.par.allreduce_grads_multi([(g, cnt, atot), (gG, ccnt, ctot)])
         self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))
         self.optimizer_critic.apply_gradients(zip(gG, self.model_critic.NN_value_grad.trainable_variables()))
+        done = torch.cuda.Event()  # every reader of this set's static inputs is behind this point
+        done.record()
+        self._set_done[self._parity] = done
+        self._parity = (self._parity + 1) % GRAPH_SETS
 
     def train_step_actor(self, train_data, total=None):
         g = self._grads("actor", lambda d: self.grad_actor(
