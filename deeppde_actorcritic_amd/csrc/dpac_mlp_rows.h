@@ -116,9 +116,14 @@ __device__ __forceinline__ bool td_prefetch(const MrArgs<T>& a, int64_t row0, in
   return true;
 }
 
+// rows_live <= 0 (a 16-row block of the split-fp16 forward's last workgroup past the last row):
+// nothing to do.  Round 5: such a block used to read its first row's sigma dw anyway, past the
+// end of dw (and of x, u for LQR_var) — an out-of-bounds read that faults only when the rows end
+// near the end of mapped memory (seen once, tests/test_gpu_td_fused.py, LQR d = 4).
 template <typename T, int ROWS>
 __device__ __forceinline__ void td_dot_rows(const MrArgs<T>& a, const T* G, int64_t row0, int rows_live,
                                             int d, int tid, bool have_pre, const T (&pre)[kTdPre]) {
+  if (rows_live <= 0) return;  // uniform over the call's threads
   const int l16 = tid % 16, P = a.td_p, M = (d + P - 1) / P;
   for (int rr = tid / 16; rr < ROWS; rr += kMrThreads / 16) {
     const int64_t r = row0 + (rr < rows_live ? rr : 0);

@@ -119,3 +119,39 @@ def test_fused_td1_rejects_mismatched_network():
                  ctypes.c_void_p(rows.data_ptr()), 20, ctypes.c_void_p(u.data_ptr()),
                  ctypes.c_void_p(data.dw.data_ptr()), ctypes.c_void_p(rows.data_ptr()), None,
                  ops._stream(rows))
+
+
+@pytest.mark.parametrize("name,d", [("LQR", 4), ("LQR_var", 10)])
+def test_fused_td1_dead_row_blocks_read_nothing_past_the_end(name, d):
+    """Round 5 regression: the split-fp16 forward's last 64-row workgroup computes the TD1 dots
+    in 16-row blocks, and a block wholly past the last row used to read its first row's sigma dw
+    (and x, u for LQR_var) anyway — past the end of those arrays (seen once as a GPU fault in
+    this file's LQR d = 4 case).  Here the rows end 48 rows into the last workgroup (three dead
+    blocks) and x, u, dw are views ending exactly at the end of their own 2 MiB-rounded
+    allocations, so any read past them leaves the allocation; the dots must agree with
+    sum_j (sigma dw)_j G_j formed from the unfused forward's G within f32 rounding."""
+    set_floatx("float32")
+    cfg = full_config(name, d, N=8, hidden=(200, 200, 200), dtype="float32")
+    bp = getattr(peq, name)(cfg.eqn_config)
+    net = psol.DeepNN(cfg, "critic_grad", torch.Generator().manual_seed(4), torch.float32, "cuda")
+    view = net.mlp_view()
+    R = 64 * 9 + 16  # the last workgroup holds 16 live rows and 48 dead ones
+    gen = torch.Generator(device="cuda").manual_seed(9)
+
+    def at_end(cols):
+        nbytes = R * cols * 4
+        cap = (nbytes + 2 ** 21 - 1) // 2 ** 21 * 2 ** 21
+        buf = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        v = buf[cap - nbytes:].view(torch.float32).view(R, cols)
+        v.copy_(torch.randn(R, cols, generator=gen, device="cuda") * 0.5)
+        return v, buf
+    (x, bx), (u, bu), (dw, bd) = at_end(d), at_end(bp.control_dim), at_end(d)
+    eqp = bp.params()
+    gdot, _ = ops.mlp_rows_td1(eqp, view, x, u, dw, save=True)
+    G, _ = ops.mlp_rows(view, x, save=True)
+    sig = ops.equation_eval(eqp, _lib.EVAL_SIGMA, x, u)
+    torch.cuda.synchronize()
+    assert torch.isfinite(gdot).all()
+    ref = torch.sum(sig * dw * G, 1)  # another summation order than the kernel's DPP tree
+    assert torch.allclose(gdot, ref, rtol=1e-5, atol=1e-6)
+    del bx, bu, bd
