@@ -204,16 +204,17 @@ inline bool pg_merge() {
   const char* e = getenv("DPAC_PG_MERGE");  // read per launch
   return !(e && e[0] == '0');
 }
-// DPAC_PG_MERGE_IN=0: the input layer keeps its own launch
+// DPAC_PG_MERGE_IN=1: the input layer in the merged launch too (k_param_grads_x3w MODE 2).  Off
+// by default: the run-time input-layer state makes that instantiation spill 54 VGPRs (round 5).
 inline bool pg_merge_in() {
   const char* e = getenv("DPAC_PG_MERGE_IN");  // read per launch
-  return pg_merge() && !(e && e[0] == '0');
+  return pg_merge() && e && e[0] == '1';
 }
 
-template <int NTI, bool L0 = false>
+template <int NTI, bool L0 = false, int MODE = 0>
 int pgw_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s, int extra_lds = 0) {
   using PL = PgwPlan<NTI, L0>;
-  auto k = k_param_grads_x3w<NTI, L0>;
+  auto k = k_param_grads_x3w<NTI, L0, MODE>;
   const int lds = PL::kSmem + extra_lds;  // + the merged input layer's compact G_0 slots
   if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds))
@@ -275,7 +276,10 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
           int nl = in ? 1 : 0;
           while (pg_merge() && (l >= 1 || in) && l + nl <= a.L && pgw13_ok(a, l + nl)) ++nl;
           if (nl >= 2) {
-            if (int e = pgw_launch<13>(a, -(l + 8 * nl), (nch + 7) / 8 * 8 * nl, s0, in ? kPgwRawG0c : 0)) return e;
+            const int64_t g = (nch + 7) / 8 * 8 * nl;
+            if (int e = in ? pgw_launch<13, false, 2>(a, -(l + 8 * nl), g, s0, kPgwRawG0c)
+                           : pgw_launch<13, false, 1>(a, -(l + 8 * nl), g, s0))
+              return e;
             l += nl - 1;
             continue;
           }

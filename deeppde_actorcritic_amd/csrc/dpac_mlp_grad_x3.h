@@ -475,9 +475,14 @@ constexpr int kPgwRawG0c = kPgxSR * 128;  // merged launches: G_0 rows in compac
 // workgroups run the L0 variant's arithmetic at run time (BN_0 only, BN_0's sums from G_0 rows,
 // which land in compact slots after the plan's LDS: the launch adds kPgwRawG0c bytes), bitwise
 // k_param_grads_x3w<NTI, true>'s results.
-template <int NTI, bool L0 = false>
+// MODE 0: one layer (lsel >= 0); 1: a merged launch of wide / output layers; 2: a merged launch
+// that starts at the input layer (run-time L0 workgroups).  Separate instantiations: the run-time
+// L0 state costs registers the one-layer kernel does not have to spare (128 VGPRs at 1 024
+// threads; round 5 measured a 54-VGPR spill when every launch carried it).
+template <int NTI, bool L0 = false, int MODE = 0>
 __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<float> a, const int lsel) {
   using PL = PgwPlan<NTI, L0>;
+  static_assert(MODE == 0 || !L0, "merged launches use the run-time input layer");
   constexpr int KP = PL::KP, CW = kPgwCW;
   static_assert(KP <= 256, "one staging thread per feature");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // PL::kSmem bytes (dynamic)
@@ -490,9 +495,9 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   int* const s_cexp = reinterpret_cast<int*>(s_cfac + CW);
   if (x3_status_set(a.status)) return;  // fell back: the f32 kernel after this one does the work
   const int64_t bx = blockIdx.x;
-  const int nl = lsel >= 0 ? 1 : (-lsel) >> 3;
-  const int l = lsel >= 0 ? lsel : ((-lsel) & 7) + (int)((bx >> 3) % nl);
-  const int64_t chunk = lsel >= 0 ? bx : (bx / (8 * nl)) * 8 + (bx & 7);
+  const int nl = MODE == 0 ? 1 : (-lsel) >> 3;
+  const int l = MODE == 0 ? lsel : ((-lsel) & 7) + (int)((bx >> 3) % nl);
+  const int64_t chunk = MODE == 0 ? bx : (bx / (8 * nl)) * 8 + (bx & 7);
   if (chunk * a.rows_per_chunk >= a.rows) return;  // past the last chunk (merged grid), before any barrier
   bool bad = false;
   const int K = a.width[l], H = a.width[l + 1];
@@ -503,7 +508,7 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   const int64_t r_begin = chunk * a.rows_per_chunk;
   const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
   const bool last = l == a.L;
-  const bool rt0 = !L0 && l == 0;   // the input layer inside a merged launch (see above)
+  const bool rt0 = MODE == 2 && l == 0;   // the input layer inside a merged launch (see above)
   const bool in0 = L0 || rt0;
   const float* srcA = in0 ? a.x : a.z + a.zoff[l];  // L0: the network input (l = 0)
   const int64_t ldA = in0 ? a.ldx : a.ztot;
