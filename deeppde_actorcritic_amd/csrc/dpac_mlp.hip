@@ -192,9 +192,11 @@ inline bool pgw13_ok(const PgArgs<float>& a, int l) {
   const int K = a.width[l], H = a.width[l + 1];
   if (K <= 128 || K > 208 || K % 4 != 0 || a.zoff[l] % 4 != 0) return false;
   if (pgx_w_ok(a, l)) return true;
+  // the output layer joins only with DPAC_PG_MERGE_OUT=1: on the merged-group kernel it is slower
+  // than on its own 8-wavefront kernel (round 5: all layers 467 vs 447 us at 204 800 rows)
+  const char* e = getenv("DPAC_PG_MERGE_OUT");
   return l == a.L && H <= 32 && H % 4 == 0 && a.ztot % 4 == 0 && a.zoff[l + 1] % 4 == 0 &&
-         (reinterpret_cast<uintptr_t>(a.z) & 15) == 0 && (getenv("DPAC_PG_MERGE_OUT") == nullptr ||
-                                                          getenv("DPAC_PG_MERGE_OUT")[0] != '0');
+         (reinterpret_cast<uintptr_t>(a.z) & 15) == 0 && e && e[0] == '1';
 }
 
 static_assert(PgwPlan<13>::kSmem + kPgwRawG0c <= 160 * 1024, "a merged launch from the input layer fits the LDS");
