@@ -255,6 +255,8 @@ int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   return pgx_launch<13, 1, 1, false>(a, l, grid, s);
 }
 
+constexpr int64_t kFallbackBlocksPg = 256;  // the guarded f32 parameter-gradient fallback's grid
+
 template <typename T>
 int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x, int64_t ldx,
            const void* z, const void* G, void* ws, void* out, hipStream_t s0) {
@@ -301,9 +303,10 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
           f.guard = net.status;
           int hmax = 0;
           for (int l = 0; l <= a.L; ++l) hmax = std::max(hmax, a.width[l + 1]);
-          hipLaunchKernelGGL((k_param_grads<float, 16, 2, 1>), dim3((unsigned)nch, (unsigned)((hmax + 127) / 128),
-                                                                   (unsigned)(a.L + 1)),
-                             dim3(kPgThreads), 0, s0, f, -1);
+          const int ngrp = (hmax + 127) / 128;  // 128-column groups of <16, 2, 1>
+          hipLaunchKernelGGL((k_param_grads<float, 16, 2, 1>),
+                             dim3((unsigned)std::min<int64_t>(nch * ngrp * (a.L + 1), kFallbackBlocksPg)),
+                             dim3(kPgThreads), 0, s0, f, -ngrp);
           if (hipError_t e = hipGetLastError()) return (int)e;
         }
         const int64_t n = a.ptot + a.width[a.L + 1];
@@ -431,7 +434,7 @@ int x3_launch(K kfn, const X3Args& a, hipStream_t s, int rows_per = kX3Rows, uin
 
 // Grid of a guarded f32 fallback launch (dpac.h dpac_mlp.status): a grid-stride pass over
 // every row tile; when the word is clear each workgroup exits after one load.
-constexpr int64_t kFallbackBlocks = 512;
+constexpr int64_t kFallbackBlocks = 256;  // one workgroup per CU (round 4: 512)
 
 template <typename T>
 int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void* out,

@@ -85,7 +85,30 @@ struct PgStage {
 // (H <= 32) WI = 4, WJ = 1, so no wavefront multiplies padding columns.
 // NTI / NTJ are compile-time: the MFMA loop is straight-line code.
 template <typename T, int NTI, int NTJ, int WI>
+__device__ __forceinline__ void pg_block(const PgArgs<T>& a, const int l, const int grp, const int64_t chunk);
+
+// l_arg >= 0: layer l_arg, chunk blockIdx.x, column group blockIdx.y.  l_arg < 0: the guarded f32
+// fallback of a split-fp16 launch over every layer, -l_arg column groups: a 1-D grid strides over
+// the (chunk, group, layer) blocks (round 5: a small grid, so the launch costs little when the
+// status word is clear and it exits at once — the (chunks x groups x layers) grid took 46 us to
+// dispatch and retire its empty workgroups on the lqr_d20 G network)
+template <typename T, int NTI, int NTJ, int WI>
 __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, const int l_arg) {
+  if (a.guard && !x3_status_set(a.guard)) return;  // a fallback launch: only once the x3 kernel fell back
+  if (l_arg >= 0) {
+    pg_block<T, NTI, NTJ, WI>(a, l_arg, (int)blockIdx.y, (int64_t)blockIdx.x);
+    return;
+  }
+  const int64_t nch = (a.rows + a.rows_per_chunk - 1) / a.rows_per_chunk, ngrp = -l_arg;
+  const int64_t nblk = nch * ngrp * (a.L + 1);
+  for (int64_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
+    if (vb != (int64_t)blockIdx.x) __syncthreads();  // the previous block's LDS reads are done
+    pg_block<T, NTI, NTJ, WI>(a, (int)(vb / (nch * ngrp)), (int)((vb / nch) % ngrp), vb % nch);
+  }
+}
+
+template <typename T, int NTI, int NTJ, int WI>
+__device__ __forceinline__ void pg_block(const PgArgs<T>& a, const int l, const int grp, const int64_t chunk) {
   using MF = Mfma<T>;
   constexpr int WJ = 4 / WI;
   constexpr int SR = PgCfg<T>::SR;
@@ -98,16 +121,12 @@ __global__ __launch_bounds__(kPgThreads) void k_param_grads(const PgArgs<T> a, c
   constexpr uint32_t ES = sizeof(T);
   __shared__ T sA[SR * LDA];
   __shared__ T sB[SR * LDB];
-  if (a.guard && !x3_status_set(a.guard)) return;  // a fallback launch: only once the x3 kernel fell back
-  const int l = l_arg >= 0 ? l_arg : (int)blockIdx.z;  // l_arg < 0: every layer, one per grid z
-  const int grp = blockIdx.y;
   const int K = a.width[l], H = a.width[l + 1];
   const int col0 = grp * CW;
   if (col0 >= H) return;  // whole workgroup: no barrier reached yet
   const int tid = threadIdx.x, lane = tid % 64;
   const int wave = __builtin_amdgcn_readfirstlane(tid / 64);
   const int wi = wave / WJ, wj = wave % WJ;
-  const int64_t chunk = blockIdx.x;
   const int64_t r_begin = chunk * a.rows_per_chunk;
   const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
   const bool first = l == 0 && grp == 0;  // also sums BN_0
