@@ -552,6 +552,8 @@ class ActorCriticSolver(object):
             return Equation.to_native((x0[off:off + cnt], dw[off:off + cnt], xb[off:off + cnt]), self.dtype)
         self._calls += 1
         key = (self.seed * 0x9E3779B1 + self._calls) & 0xFFFFFFFFFFFFFFFF
+        if out is None:
+            return self.bsde.sample_device(kind, cnt, N, key, off, self.dtype)
         return self.bsde.sample_device(kind, cnt, N, key, off, self.dtype, out=out)
 
     def sample_iteration(self, num_sample, N_critic, N_actor):

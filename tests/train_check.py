@@ -88,9 +88,13 @@ def main():
         if a.sampler == "device":  # same Philox keys in every run; increments drawn in float64
             draw = bsde.sample_device
 
-            def sample64(kind, n, N, key, off=0, dtype=None, _draw=draw, _dt=sp.dtype):
+            def sample64(kind, n, N, key, off=0, dtype=None, out=None, _draw=draw, _dt=sp.dtype):
                 b = _draw(kind, n, N, key, off, torch.float64)
-                return type(b)(*(t.to(_dt) for t in b))
+                if out is None:
+                    return type(b)(*(t.to(_dt) for t in b))
+                for dst, src in zip(out, b):  # the solver's in-place prefetch (its idle graph set)
+                    dst.copy_(src)
+                return out
             bsde.sample_device = sample64
         if init is None:  # every run starts from the first run's weights, in float64
             init = {"critic": sp.model_critic.NN_value.export_params(),
