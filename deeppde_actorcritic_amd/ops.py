@@ -352,12 +352,16 @@ class _ActorRolloutNN(torch.autograd.Function):
 
 def actor_rollout_saves(eqp, scheme: int, x0, dw, total_time: float, num_steps: int, net):
     """The actor's rollout with `net` as control and the backward saves, no autograd:
-    (y [B], disc_N [B], x_N [B, d], saved) with saved = (x, u, dw, z, flag, disc_t, mask) as
-    actor_bptt_grads takes it (the forward of _ActorRolloutNN)."""
+    (y [B], disc_N [B], x_N [B, d], saved) with saved = (x, u, dw, z, flag, disc_t, mask,
+    prepared) as actor_bptt_grads takes it (the forward of _ActorRolloutNN).  prepared = the
+    network's forward AND backward images from one dpac_mlp_prepare launch (round 5: the
+    backward's images are formed here, beside the critic step, not in front of the BPTT —
+    the actor's parameters do not change in between)."""
+    prepared = net.mlp_prepared()
     x, dt, coef, u, y, disc, (z, flag, disc_t, mask) = rollout_nn(
-        eqp, scheme, x0, dw, total_time, num_steps, net.mlp_view(), cost_order=_lib.COST_ACTOR,
+        eqp, scheme, x0, dw, total_time, num_steps, prepared[0], cost_order=_lib.COST_ACTOR,
         save=True)
-    return y, disc, x[num_steps], (x, u, dw.contiguous(), z, flag, disc_t, mask)
+    return y, disc, x[num_steps], (x, u, dw.contiguous(), z, flag, disc_t, mask, prepared)
 
 
 def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_xN):
@@ -366,11 +370,15 @@ def actor_bptt_grads(eqp, scheme, T, N, ekn, rs, params, saved, g_y, g_disc, g_x
     the BPTT of solver.py:92-97 (dpac_rollout_nn_bwd, then dpac_mlp_param_grads)."""
     x, u, dw, z, flag, disc_t = saved[:6]
     mask = saved[6] if len(saved) > 6 else None
+    prepared = saved[7] if len(saved) > 7 else None  # the forward's images of the same parameters
     L = (len(params) - 1) // 3 - 1
     gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
     B, d = x.shape[1], x.shape[2]
     widths = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
-    view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, ekn, BPTT_MODE == "fused")
+    if prepared is not None and BPTT_MODE == "fused":
+        view, wt, wt_km = prepared
+    else:
+        view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, ekn, BPTT_MODE == "fused")
     s = view.scales
     zoff = np.cumsum([0] + widths[1:]).tolist()
     zl = [None] + [z[:, :, zoff[i - 1]:zoff[i]] for i in range(1, L + 2)]

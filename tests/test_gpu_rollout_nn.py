@@ -328,7 +328,7 @@ def test_bptt_stager_writer_kernel_bitwise(name, d, hidden, B, dtype, scheme):
     sch = SCHEMES[scheme]
     x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=8, dtype=dtype, device=DEV)
     y, disc, xN, saved = ops.actor_rollout_saves(eqp, sch, x0, dw, T, N, net)
-    x, u, dwc, z, flag, disc_t, _ = saved
+    x, u, dwc, z, flag, disc_t = saved[:6]
     params = [p.detach() for p in net.trainable_variables()]
     L = len(hidden)
     gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]

@@ -58,7 +58,7 @@ def main():
         sch = _lib.SCHEME_ADAPTIVE
         fwd = lambda: ops.actor_rollout_saves(eqp, sch, x0, dw, 0.2, N, net)
         y, disc, xN, saved = fwd()
-        x, u, dwc, z, flag, disc_t, mask = saved
+        x, u, dwc, z, flag, disc_t, mask = saved[:7]
         params = net.trainable_variables()
         L = 3
         gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]

@@ -65,7 +65,7 @@ def main():
     torch.cuda.synchronize()
     steps = np.arange(8, 62)
     res = {"B": B, "N": N, "fwd": table(lib, 8, FWD_POINTS, steps)}
-    x, u, dwc, z, flag, disc_t, mask = saved
+    x, u, dwc, z, flag, disc_t, mask = saved[:7]
     params = net.trainable_variables()
     L = 3
     gam, bet, Ws, b = params[:L + 2], params[L + 2:2 * L + 4], params[2 * L + 4:3 * L + 5], params[-1]
