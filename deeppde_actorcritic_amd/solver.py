@@ -531,6 +531,7 @@ class ActorCriticSolver(object):
         self._gsets = {}          # (B, N_critic, N_actor) -> [(actor graphs, critic graphs)] * 2
         self._parity = 0          # the set the next train_iteration uses
         self._set_done = [None, None]  # event after the last iteration that used each set
+        self._consts = {}  # constant operands of the graphs (never written)
 
     # ---- variables ---------------------------------------------------------
     def critic_variables(self):
@@ -676,7 +677,10 @@ class ActorCriticSolver(object):
                 v = self.model_critic.NN_value(xl, False, const_params=True)[:, 0]
                 gV, = torch.autograd.grad(v.sum(), xl)
             term = v.detach()
-        g_y = torch.full_like(y, 1.0 / B)
+        key = ("g_y", B, y.dtype, y.device)
+        g_y = self._consts.get(key)
+        if g_y is None:  # made in the warm-up before a graph capture: the graph reads it, no fill kernel
+            g_y = self._consts[key] = torch.full_like(y, 1.0 / B)
         g_disc = term / B
         g_xN = gV * (disc / B).unsqueeze(1)
         net = self.model_actor.NN_control
