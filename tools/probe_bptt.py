@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--only", default="fwd,bwd,pg")
+    ap.add_argument("--dump", default=None, help="save the forward's and the BPTT's outputs (torch.save) for a "
+                                                 "bitwise A/B of two builds (tools/cmp_dumps.py)")
     a = ap.parse_args()
     from deeppde_actorcritic_amd import _lib, ops
     from deeppde_actorcritic_amd import equation as peq
@@ -72,6 +74,9 @@ def main():
                                       g_xN, g_disc, g_y, mask)
         G = bwd()
         Gall = ops.G_all(G)
+        if a.dump:
+            torch.save({"y": y, "disc": disc, "xN": xN, "x": x, "u": u, "z": z, "mask": mask, "G": Gall},
+                       f"{a.dump}_{B}.pt")
         pg = lambda: ops.mlp_param_grads(view, x[:N].reshape(N * B, 20), z.reshape(N * B, -1),
                                          Gall.reshape(N * B, -1), params)
         out = {"B": B, "N": N, "dtype": a.dtype}
