@@ -54,6 +54,14 @@ PgArgs<T> pg_args(const dpac_mlp& net, int64_t rows, const void* x, int64_t ldx,
 #ifndef DPAC_PG_MIN_ROWS
 #define DPAC_PG_MIN_ROWS 256  // rows per chunk at least: small row counts (the critic's V over 3B rows)
 #endif                        // would otherwise write and re-read ~256 near-empty partials
+// DPAC_PG_MIN_ROWS in the environment overrides the floor (timing comparisons; read per call, so
+// a process must keep one value between sizing its workspace and launching)
+inline int64_t pg_min_rows() {
+  const char* e = getenv("DPAC_PG_MIN_ROWS");
+  const long long v = e ? atoll(e) : 0;
+  return v >= 16 ? (int64_t)v : (int64_t)DPAC_PG_MIN_ROWS;
+}
+
 template <typename T>
 int64_t pg_chunk_rows(int64_t rows, int64_t max_ld) {
   // DPAC_PG_CHUNKS chunks of at least DPAC_PG_MIN_ROWS rows: the wide layers' two column
@@ -62,7 +70,7 @@ int64_t pg_chunk_rows(int64_t rows, int64_t max_ld) {
   // them below 2 GiB.
   constexpr int SR = PgCfg<T>::SR;
   int64_t per = (rows + DPAC_PG_CHUNKS - 1) / DPAC_PG_CHUNKS;
-  per = std::max<int64_t>(per, DPAC_PG_MIN_ROWS);
+  per = std::max<int64_t>(per, pg_min_rows());
   const int64_t cap = (((int64_t)1 << 31) - 1) / (max_ld * (int64_t)sizeof(T)) / SR * SR;
   per = (per + SR - 1) / SR * SR;
   return std::max<int64_t>(std::min(per, cap), SR);

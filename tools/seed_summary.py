@@ -49,6 +49,25 @@ def main():
                 summary[k + "_within_1e-3"] = dm < 1e-3
                 if sds:
                     summary[k + "_diff_over_max_seed_sd"] = dm / max(sds)
+        # paired: the same seed (same initial weights, same Philox increments) in both precisions
+        by = {n: {r["seed"]: r for r in runs[n]} for n in ("gpu32", "gpu64")}
+        common = sorted(set(by["gpu32"]) & set(by["gpu64"]), key=int)
+        for k in ("err_value", "err_control"):
+            key = k + "_final_mean"
+            v32 = [r[key] for r in runs["gpu32"]]
+            v64 = [r[key] for r in runs["gpu64"]]
+            if len(v32) > 1 and len(v64) > 1:  # unpaired: Welch's standard error of the difference of means
+                se = (statistics.variance(v32) / len(v32) + statistics.variance(v64) / len(v64)) ** 0.5
+                summary[k + "_unpaired"] = {"n32": len(v32), "n64": len(v64),
+                                            "diff_of_means": statistics.mean(v32) - statistics.mean(v64),
+                                            "se": se, "diff_of_medians": statistics.median(v32) - statistics.median(v64)}
+            d = [by["gpu32"][s_][key] - by["gpu64"][s_][key] for s_ in common]
+            if len(d) > 1:
+                sd = statistics.stdev(d)
+                summary[k + "_paired"] = {"seeds": common, "diffs": d, "mean": statistics.mean(d), "sd": sd,
+                                          "se": sd / len(d) ** 0.5, "median": statistics.median(d),
+                                          "max_abs": max(abs(x) for x in d),
+                                          "mean_within_1e-3": abs(statistics.mean(d)) < 1e-3}
     json.dump(summary, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in summary.items() if k != "runs"}, indent=1))
 
