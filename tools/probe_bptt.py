@@ -68,6 +68,7 @@ def main():
         view, wt, wt_km = ops.mlp_prepare([p.detach() for p in gam], [p.detach() for p in bet],
                                           [p.detach() for p in Ws], b.detach(), False, True)
         g_y = torch.full_like(y, 1.0 / B)
+        torch.manual_seed(B)  # the same dL/d(disc), dL/dx_N in every process (--dump A/B)
         g_disc = torch.rand_like(y) / B
         g_xN = torch.randn_like(xN) / B
         bwd = lambda: ops._bptt_fused(eqp, sch, 0.2, N, L, x, u, dwc, z, flag, disc_t, view, wt, wt_km, widths,
