@@ -198,7 +198,11 @@ def test_fp32_production_training_vs_oracle_vectors(path):
     np.random.seed(seed_np)
     hist = sp.train()[0]
     assert sp._actor_split_ok() and sp._critic_split_ok()
-    assert {k[0] for k in sp._graphs} == {"actor_split", "critic_split"}
+    # the split graphs (round 5: psol.GRAPH_SETS alternating sets, solver.train_iteration), and no
+    # unsplit gradient graph
+    sets = [s for v in sp._gsets.values() for s in v if s is not None]
+    assert len(sets) == psol.GRAPH_SETS and not sp._graphs
+    assert all(isinstance(a, psol._SplitActorGraphs) and isinstance(c, psol._SplitCriticGraphs) for a, c in sets)
     ref = g["history"]
     assert hist.shape == ref.shape
     d_val = np.abs(hist[:-1, 3] - ref[:-1, 3])
