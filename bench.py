@@ -21,7 +21,11 @@ MALL-resident) is the variant `rollout_mall_resident`, run only with --mall: it 
 same kernel, and without it every launch of the headline kernel in a default run is a cold
 one, so a rocprofv3 summary of the driver's command averages exactly the headline's launches.
 Trajectories shard across ranks by global index (weak scaling, no collective on
-the data path).  Rank 0 prints ONE JSON line.
+the data path).  Beside the weak-scaling headline the line carries `strong_scaling` (the same
+rollout with the GLOBAL batch fixed at 4096 and split over the ranks by parallel.shard_range,
+SURVEY §8(d)) and `speedup_vs_1`: both figures divided by the one-GPU figure, which rank 0
+measures alone inside the same job (the other ranks wait at a barrier), so the driver's 1->8
+run reads a measured speed-up, not one true by construction.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -41,10 +45,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "SDE trajectory-steps/sec (batch×horizon) at d=20; value-fn rel-L2 vs analytic"
 B_PER_GPU, DIM, HORIZON, T_TOTAL = 4096, 20, 200, 0.2
+B_STRONG = 4096  # strong scaling: the global batch, split over the ranks
 N_SETS = 5  # rotating buffer sets: 5 x 138 MB (f32) > the 256 MiB Infinity Cache
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (f32-in MFMA) dense peak
 MFMA_F16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA dense peak (~2.5 PF)
+MFMA_F64_PEAK_TFS = 78.6  # AMD's MI355X spec: FP64 matrix dense peak (not in the guide)
 MLP_FLOP_PER_ROW = 2 * (20 * 200 + 200 * 200 * 2 + 200 * 20)  # 176 000
 
 
@@ -159,6 +165,8 @@ def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total
     for _ in range(warmup):
         iteration()
     torch.cuda.synchronize()
+    if par is not None:
+        par.timings = []  # the gradient all-reduces of the timed iterations
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(iters):
@@ -166,6 +174,18 @@ def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total
     torch.cuda.synchronize()
     barrier(world)
     ms = max_over_ranks(time.perf_counter() - t0, world) / iters * 1e3
+    coll = None
+    if par is not None:
+        tm, par.timings = par.timings, None
+        ev_ms = sum(a.elapsed_time(b) for a, b, _ in tm) / iters
+        coll = {"allreduces_per_iteration": len(tm) / iters,
+                "allreduce_ms_per_iteration": max_over_ranks(ev_ms, world),
+                "allreduce_host_ms_per_iteration": max_over_ranks(sum(h for _, _, h in tm) / iters * 1e3, world),
+                "bytes_per_iteration": None if not tm else sum(
+                    p.numel() * p.element_size() for p in sp.critic_variables() + sp.actor_variables()),
+                "note": "HIP events on the calling stream around each dist.all_reduce of the timed "
+                        "iterations (parallel.DataParallel.timings), summed per iteration, max over ranks; "
+                        "host_ms: the Python call's wall time"}
     # MLP work per iteration, in forward-pass equivalents (176 kFLOP per row at d = 20) per
     # trajectory-step: EXECUTED by this build = 7 (actor forward in the critic's rollout, G
     # forward, G backward chain + G parameter gradients = 2, actor forward with saves,
@@ -176,7 +196,7 @@ def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total
             "mlp": "20-200-200-200-%d" % cfg.eqn_config.control_dim, "ms_per_iteration": ms,
             "traj_steps_per_s": 2 * Bg * N / (ms * 1e-3),
             "mlp_executed_TFLOPs": 7 * rate, "mlp_reference_equiv_TFLOPs": 11 * rate,
-            "mlp_math": ops_mlp_math(dtype)}
+            "mlp_math": ops_mlp_math(dtype), "collectives": coll}
 
 
 def ops_mlp_math(dtype):
@@ -341,6 +361,40 @@ def launch_ranks(n, argv):
     return proc.wait()
 
 
+def strong_scaling(lib, eqp, scheme, dtype, rank, world, args, value, ms_per_step, esize, solo_value):
+    """The headline rollout with the GLOBAL batch fixed at B_STRONG = 4096 trajectories, split
+    over the ranks by parallel.shard_range (rank r rolls out global trajectories
+    [offset_r, offset_r + count_r): trajectories are independent, equation.py:53-69), the same
+    N_SETS cold buffer sets, barrier + synchronize wall clock, max over ranks.  frac is the
+    algorithmic bytes over the wall time against the aggregate HBM peak of the world's GPUs.
+    At N = 1 it is the headline itself (B_STRONG = B_PER_GPU)."""
+    from deeppde_actorcritic_amd.parallel import shard_range
+    N, d = HORIZON, DIM
+    off, cnt = shard_range(B_STRONG, rank, world)
+    per_gpu = [shard_range(B_STRONG, r, world)[1] for r in range(world)]
+    if world == 1 and B_STRONG == B_PER_GPU:
+        wall_ms = ms_per_step
+    else:
+        progress(f"strong scaling: global batch {B_STRONG}, {cnt} trajectories on rank {rank}")
+        rs = RolloutSets(lib, eqp, scheme, dtype, cnt, N, d, off, N_SETS)
+        wall, _ = time_launches(rs.launcher(N_SETS), args.steps, args.warmup, world)
+        wall_ms = max_over_ranks(wall, world) / args.steps * 1e3
+        del rs
+    v = B_STRONG * N / (wall_ms * 1e-3)
+    achieved = B_STRONG * N * (2 * d + 2) * esize / (wall_ms * 1e-3) / 1e9
+    return {"value": v, "unit": "traj-steps/s", "ms_per_step": wall_ms, "scaling": "strong",
+            "global_batch": B_STRONG, "batch_per_gpu": max(per_gpu), "batch_per_rank": per_gpu,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                         "frac": achieved / (HBM_PEAK_GBS * world),
+                         "note": "algorithmic bytes (168 B per trajectory-step) of the whole 4096-trajectory "
+                                 "batch / the max-over-ranks wall time per step, against the world's "
+                                 "aggregate HBM peak"},
+            "note": "each trajectory is a sequential 200-step chain on one 16-lane group, and at B = 4096 "
+                    "one GPU already runs one wavefront per SIMD, so a rank's shard takes about the per-wave "
+                    "chain latency whatever its size: strong scaling of THIS batch is latency-bound "
+                    "(variants.strong_scaling_shard_proxy times the shards on one GPU)"}
+
+
 def check_world(args, world):
     """Every rank: the launcher's world size is the --gpus asked for, and (RCCL) each rank has
     a GPU of its own.  DPAC_DIST_BACKEND=gloo is the rehearsal mode in which ranks may share
@@ -368,6 +422,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--no-train", action="store_true", help="skip the training-iteration variants")
+    ap.add_argument("--strong-proxy", action="store_true",
+                    help="also time the strong-scaling shards (B = 4096 / 2, 4, 8) on this one GPU")
     ap.add_argument("--mall", action="store_true",
                     help="also time the MALL-resident one-set loop (same kernel as the headline)")
     args = ap.parse_args()
@@ -386,7 +442,11 @@ def main():
         assert dist.get_world_size() == world
     else:
         torch.cuda.set_device(0)
-    devices = min(visible, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    devices = min(visible, local_world)  # this node's GPUs in use
+    # ranks share a GPU only when this node runs more ranks than it has GPUs (the gloo
+    # rehearsal); a multi-node launch has world > the node's GPUs with one rank per GPU
+    shared = world > 1 and local_world > visible
 
     from deeppde_actorcritic_amd import _lib, ops
     from deeppde_actorcritic_amd.equation import LQR
@@ -406,6 +466,22 @@ def main():
     ms_per_step = wall / args.steps * 1e3
     value = world * B * N * args.steps / wall
     algo_bytes = B * N * (2 * d + 2) * esize
+    # the one-GPU figure of the same job: rank 0 alone (the others wait at a barrier), the same
+    # B = 4096 batch, launches and timer; at N = 1 it is the headline itself
+    if world > 1:
+        barrier(world)
+        if rank == 0:
+            progress("one-GPU reference: rank 0 alone")
+            solo_wall, _ = time_launches(rs.launcher(N_SETS), args.steps, args.warmup, 1)
+            solo_value = B * N * args.steps / solo_wall
+        else:
+            solo_value = 0.0
+        barrier(world)
+        solo_value = max_over_ranks(solo_value, world)
+    else:
+        solo_value = value
+    strong = strong_scaling(lib, eqp, scheme, dtype, rank, world, args, value, ms_per_step, esize,
+                            solo_value)
     # the same timer as `value`: the wall clock over the K launches (max over ranks) / K
     achieved = algo_bytes / (ms_per_step * 1e-3) / 1e9
     achieved_ev = algo_bytes / (per_launch_ms * 1e-3) / 1e9
@@ -425,7 +501,14 @@ def main():
                  "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else (
                      "external" if world > 1 else None),
                  "note": ("ranks share a GPU: DPAC_DIST_BACKEND=gloo rehearsal, not a scaling figure"
-                          if world > devices else "one rank per GPU")},
+                          if shared else "one rank per GPU")},
+        "strong_scaling": strong,
+        "speedup_vs_1": {"weak": value / solo_value, "strong": strong["value"] / solo_value,
+                         "one_gpu_value": solo_value, "unit": "traj-steps/s",
+                         "note": "one_gpu_value: B = 4096 on ONE GPU (rank 0 alone inside this job, the "
+                                 "same launches and wall timer; at N = 1 the headline itself); weak = "
+                                 "value / one_gpu_value (B = 4096 per GPU), strong = strong_scaling.value / "
+                                 "one_gpu_value (B = 4096 in all)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": tsrc, "kernel": "dpac::k_rollout_staged",
@@ -435,9 +518,9 @@ def main():
                      "note": "achieved = algorithmic bytes (168 B per trajectory-step) / ms_per_step, the "
                              "wall clock that gives `value` (barrier + synchronize around the K launches, "
                              "max over ranks); event_pair: the HIP event pair over the same launches on the "
-                             "launch stream.  Every launch of this kernel in a default run is an HBM-cold one, "
-                             "so rocprofv3 --stats of the same command averages them "
-                             "(tools/rocprof_headline.py -> profiles/r04_rocprof_headline.json)"},
+                             "launch stream.  Every launch of this kernel in a default run (N = 1) is an "
+                             "HBM-cold one, so rocprofv3 --stats of the same command averages them "
+                             "(tools/rocprof_headline.py -> profiles/r06_rocprof_headline.json)"},
     }
     if not args.no_variants:
         progress("variants: in-kernel Philox, float64, TD1, fused NN rollout" + (", MALL-resident" if args.mall else ""))
@@ -456,6 +539,43 @@ def main():
         variants["rollout_inkernel_philox"] = {
             "traj_steps_per_s": world * B * N * k2 / max_over_ranks(w2, world),
             "avg_launch_ms": pl2, "hbm_GBps_algorithmic": B * N * (d + 2) * esize / (pl2 * 1e-3) / 1e9}
+        # the device sampler (k_sample_dw, equation.py:13-23's draws) at the bench shape, writing
+        # x0, dw [N, B, d] and x_bdry: (N + 2)·B·d elements per call
+        sbufs = [tuple(torch.empty(t.shape, dtype=dtype, device=t.device) for t in (st[0], st[1], st[0]))
+                 for st in rs.sets]
+
+        def sample_launch(i):
+            x0s, dws, xbs = sbufs[i % N_SETS]
+            ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=99 + i, traj_offset=off, dtype=dtype,
+                       device=x0s.device, out=(x0s, dws, xbs))
+        w6, pl6 = time_launches(sample_launch, k2, 5, world)
+        sbytes = (N + 2) * B * d * esize
+        variants["sample_normal_device"] = {
+            "kernel": "dpac::k_sample_dw (+ the x0 / x_bdry launch)", "traj_steps_per_s":
+            world * B * N * k2 / max_over_ranks(w6, world), "avg_call_ms": pl6,
+            "roofline": {"bound": "hbm", "achieved": sbytes / (pl6 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": sbytes / (pl6 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_call": sbytes},
+            "note": "ops.sample into the bench's cold buffer sets (Philox4x32-10 normals, every generated "
+                    "normal used): the bytes written over the HIP event pair per call"}
+        del sbufs
+        if args.strong_proxy and world == 1:
+            # what a rank of the strong-scaling run computes, timed on this one GPU: the
+            # 4096-trajectory batch's shard for 2, 4 and 8 ranks
+            from deeppde_actorcritic_amd.parallel import shard_range
+            prox = {}
+            for g in (2, 4, 8):
+                cnt = shard_range(B_STRONG, 0, g)[1]
+                rsg = RolloutSets(lib, eqp, scheme, dtype, cnt, N, d, 0, N_SETS)
+                wg, _ = time_launches(rsg.launcher(N_SETS), args.steps, args.warmup, 1)
+                del rsg
+                msg = wg / args.steps * 1e3
+                prox[f"gpus_{g}"] = {"batch_per_gpu": cnt, "ms_per_step": msg,
+                                     "predicted_strong_speedup": ms_per_step / msg}
+            variants["strong_scaling_shard_proxy"] = {
+                "shards": prox, "note": "one rank's shard of the 4096-trajectory batch timed alone on one "
+                                        "GPU (no collective exists on this path, so a rank's time is its "
+                                        "shard's); predicted speed-up = the headline's ms_per_step / the shard's"}
         # the reference's own precision (float64, main.py:35): 336 B per traj-step
         if dtype == torch.float32:
             rs64 = RolloutSets(lib, eqp, scheme, torch.float64, B, N, d, off, N_SETS)
@@ -510,17 +630,24 @@ def main():
         flops = MLP_FLOP_PER_ROW * B * N
         tfs = flops / (pl4 * 1e-3) / 1e12
         x3 = dtype == torch.float32 and ops.MLP_MATH == "x3"
+        peak_nn = MFMA_F16_PEAK_TFS / 3 if x3 else (MFMA_F32_PEAK_TFS if dtype == torch.float32
+                                                     else MFMA_F64_PEAK_TFS)
         variants["rollout_nn_fused"] = {
             "traj_steps_per_s": world * B * N * k4 / max_over_ranks(w4, world), "avg_launch_ms": pl4,
             "mlp": "20-200-200-200-20", "mlp_math": ops_mlp_math(dtype),
-            "roofline": {"bound": "mfma", "achieved": tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": tfs / MFMA_F32_PEAK_TFS,
+            # the primary peak is the ceiling of the instruction the kernel runs: split-fp16 products
+            # (3 fp16 MFMAs per f32 product) -> the fp16 dense peak / 3 in f32-equivalent
+            # flops; the exact-f32 kernels -> the f32-input MFMA peak
+            "roofline": {"bound": "mfma", "achieved": tfs, "peak": peak_nn, "unit": "TFLOP/s",
+                         "frac": tfs / peak_nn,
                          "kernel": "dpac::k_rollout_nn_x3" if x3 else "dpac::k_rollout_nn",
-                         "note": "achieved in f32-equivalent flops (176 kFLOP per trajectory-step) against the "
-                                 "f32-input MFMA peak"
-                                 + ("; the split-fp16 products' own ceiling is the fp16 dense peak / 3 = "
-                                    f"{MFMA_F16_PEAK_TFS / 3:.0f} TFLOP/s f32-equivalent: "
-                                    f"frac {tfs / (MFMA_F16_PEAK_TFS / 3):.3f} of that" if x3 else "")}}
+                         "frac_of_f32_mfma_peak": tfs / MFMA_F32_PEAK_TFS,
+                         "note": "achieved in f32-equivalent flops (176 kFLOP per trajectory-step)"
+                                 + (f"; peak = the fp16 dense MFMA peak / 3 = {peak_nn:.0f} TFLOP/s "
+                                    "f32-equivalent, the ceiling of the split-fp16 products this kernel "
+                                    "executes; frac_of_f32_mfma_peak compares with the f32-input MFMA "
+                                    "(157.3 TFLOP/s), which it does not execute" if x3 else
+                                    "; peak = the f32-input MFMA peak")}}
         del rs, nn_out
         torch.cuda.empty_cache()
         if not args.no_train:
@@ -544,6 +671,17 @@ def main():
             v["collective"] = ((f"two gradient all-reduces per iteration ({v['backend']}; nccl = RCCL "
                                 "over xGMI): V's, then the actor's and G's in one flattened exchange")
                                if world > 1 else None)
+            if world > 1:  # the same global batch on ONE GPU: rank 0 alone, inside this job
+                del par
+                torch.cuda.empty_cache()
+                barrier(world)
+                one = training_variant("lqr_var_d20", dtype, 16384, 1, iters=4) if rank == 0 else None
+                barrier(world)
+                one_ms = max_over_ranks(one["ms_per_iteration"] if one else 0.0, world)
+            else:
+                one_ms = v["ms_per_iteration"]
+            v["ms_per_iteration_1gpu"] = one_ms
+            v["speedup_vs_1"] = one_ms / v["ms_per_iteration"]
             variants["training_dp_lqr_var_d20"] = v
         out["variants"] = variants
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

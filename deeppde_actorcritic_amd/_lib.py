@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPAC_LIB", os.path.join(_HERE, "libdpac.so"))
 
 # constants mirrored from include/dpac.h
-ABI_VERSION = 7  # DPAC_ABI_VERSION: load() refuses a library built from another header
+ABI_VERSION = 8  # DPAC_ABI_VERSION: load() refuses a library built from another header
 DPAC_OK, DPAC_EINVAL, DPAC_EUNSUP = 0, -1, -2
 F32, F64 = 0, 1
 EQN_LQR, EQN_VDP, EQN_EKN, EQN_LQR_VAR = 0, 1, 2, 3
@@ -23,6 +23,7 @@ TD1, TD2, TD1_GDOT = 1, 2, 3
 COST_CRITIC, COST_ACTOR = 0, 1
 SAMPLE_NORMAL, SAMPLE_BOUNDED, SAMPLE_ZERO_X0 = 0, 1, 2
 X3_FELL_BACK = 1  # dpac_mlp.status bit: a split-fp16 operand left the split range (dpac.h)
+GUARD_INLINE, GUARD_SPLIT_ONLY, GUARD_FALLBACK_ONLY = 0, 1, 2  # dpac_mlp.guard_phase (dpac.h)
 (EVAL_DRIFT, EVAL_SIGMA, EVAL_W, EVAL_Z, EVAL_V_TRUE, EVAL_U_TRUE, EVAL_V_GRAD,
  EVAL_B) = range(8)
 
@@ -67,6 +68,7 @@ class Mlp(ctypes.Structure):
         ("weight_x3", ctypes.c_void_p * (MLP_MAX_HIDDEN + 1)),
         ("weight_t_x3", ctypes.c_void_p * (MLP_MAX_HIDDEN + 1)),
         ("status", ctypes.c_void_p),
+        ("guard_phase", ctypes.c_int32),
     ]
 
 

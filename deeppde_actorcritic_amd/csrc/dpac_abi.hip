@@ -106,6 +106,15 @@ int check_sample_type(int32_t st) {
   return DPAC_OK;
 }
 
+// dpac_mlp.guard_phase: one of DPAC_GUARD_*, and a split phase only with a status word
+int check_guard_phase(const dpac_mlp* net) {
+  if (net->guard_phase < DPAC_GUARD_INLINE || net->guard_phase > DPAC_GUARD_FALLBACK_ONLY)
+    return fail(DPAC_EINVAL, "guard_phase must be 0, 1 or 2 (got %d)", net->guard_phase);
+  if (net->guard_phase != DPAC_GUARD_INLINE && !net->status)
+    return fail(DPAC_EINVAL, "guard_phase %d needs a status word", net->guard_phase);
+  return DPAC_OK;
+}
+
 int check_mlp(const dpac_eqn_params* eq, const dpac_mlp* actor) {
   if (!actor) return fail(DPAC_EINVAL, "actor MLP pointer is NULL");
   const int L = actor->n_hidden;
@@ -130,7 +139,7 @@ int check_mlp(const dpac_eqn_params* eq, const dpac_mlp* actor) {
     return fail(DPAC_EINVAL, "actor: output width %d must be control_dim%s (%d)",
                 actor->width[L + 1], actor->ekn_head ? " + 1" : "",
                 eq->control_dim + actor->ekn_head);
-  return DPAC_OK;
+  return check_guard_phase(actor);
 }
 
 // A dpac_mlp for the row-parallel kernels (no equation attached).
@@ -147,7 +156,7 @@ int check_net(const dpac_mlp* net) {
       return fail(DPAC_EINVAL, "bn_scale/bn_shift[%d] is NULL", i);
   }
   if (!net->bias) return fail(DPAC_EINVAL, "bias is NULL");
-  return DPAC_OK;
+  return check_guard_phase(net);
 }
 
 #define DPAC_REQUIRE(ptr) \

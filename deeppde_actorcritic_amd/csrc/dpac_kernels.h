@@ -1276,6 +1276,7 @@ int run_op(const OpArgs& a) {
       r.mask = r.fast ? a.mask_in : nullptr;
       r.mb = nn_mask_tile_bytes(m.L);
       const dim3 ngrid((unsigned)((a.B + kNnRows - 1) / kNnRows)), nblock(kNnThreads);
+      const int gphase = m.status ? a.mlp.guard_phase : DPAC_GUARD_INLINE;  // dpac.h guard_phase
       if constexpr (kFastOk) {  // split-fp16 chain (dpac_rollout_nn_x3.h): needs the forward's mask
         // (guarded by a status word: only with the f32 fast path's operands for the fallback)
         if (r.mask && bptt_kernel() == 2 && (!m.status || r.fast) &&
@@ -1284,11 +1285,14 @@ int run_op(const OpArgs& a) {
           r.tr = nx_rows(a.B);
           auto kfn = adaptive ? k_rollout_nn_bwd_x3<E, D, DPAC_SCHEME_ADAPTIVE>
                               : k_rollout_nn_bwd_x3<E, D, DPAC_SCHEME_NAIVE>;
-          if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)NxLds::total))
-            return (int)e;
-          hipLaunchKernelGGL(kfn, dim3((unsigned)((a.B + r.tr - 1) / r.tr)), nblock, NxLds::total, s, eq, c, m, r);
-          if (m.status) {  // the f32 BPTT, run only once the x3 kernel fell back (dpac.h dpac_mlp.status)
+          if (gphase != DPAC_GUARD_FALLBACK_ONLY) {
+            if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)NxLds::total))
+              return (int)e;
+            hipLaunchKernelGGL(kfn, dim3((unsigned)((a.B + r.tr - 1) / r.tr)), nblock, NxLds::total, s, eq, c, m, r);
+          }
+          if (m.status && gphase != DPAC_GUARD_SPLIT_ONLY) {
+            // the f32 BPTT, run only once the x3 kernel fell back (dpac.h dpac_mlp.status)
             int wsum = 0;
             for (int i = 0; i <= m.L + 1; ++i) wsum += m.width[i];
             const BwdPlan<T, D, E::CDIM> pl(wsum, m.ztot, true, r.mb);
@@ -1305,6 +1309,7 @@ int run_op(const OpArgs& a) {
           break;
         }
       }
+      if (gphase == DPAC_GUARD_FALLBACK_ONLY) break;  // phase 1 did the whole work
       if (bptt_kernel() == 2) {
         int wsum = 0;
         for (int i = 0; i <= m.L + 1; ++i) wsum += m.width[i];
@@ -1371,12 +1376,14 @@ int run_op(const OpArgs& a) {
       r.save_mask = nullptr;
       r.mb = nn_mask_tile_bytes(m.L);
       const bool cost = a.y != nullptr;
+      const int gphase = m.status ? a.mlp.guard_phase : DPAC_GUARD_INLINE;  // dpac.h guard_phase
       if constexpr (std::is_same<T, float>::value) {
         // 4-row MFMA blocks (dpac_rollout_nn4.h) where the 16-row tiles would leave
         // most CUs idle: 4x4x1 costs 4x the cycles per flop of 16x16x4, and measured
         // 11.4 vs 15.4 us per step at B <= 1024, 15.8 vs 15.4 at 2048, 31 vs 15.4 at 4096
         const int tile = nn_tile_rows();
         if (tile == 4 || (tile == 0 && a.B <= 1024)) {
+          if (gphase == DPAC_GUARD_FALLBACK_ONLY) break;  // no split-fp16 launch here: nothing to redo
           const int rg = a.B <= 1024 ? 1 : 2;
           const dim3 g4((unsigned)((a.B + 4 * rg - 1) / (4 * rg))), b4(kN4Threads);
 #define DPAC_ROLL_NN4(SCH, CO, RG) \
@@ -1420,18 +1427,21 @@ int run_op(const OpArgs& a) {
   if (mask) DPAC_NX_LAUNCH(SCH, CO, true, true)                \
   else if (save) DPAC_NX_LAUNCH(SCH, CO, true, false)          \
   else DPAC_NX_LAUNCH(SCH, CO, false, false)
-          if (adaptive) {
-            if (cost) { DPAC_NX_SV(DPAC_SCHEME_ADAPTIVE, true) } else { DPAC_NX_SV(DPAC_SCHEME_ADAPTIVE, false) }
-          } else {
-            if (cost) { DPAC_NX_SV(DPAC_SCHEME_NAIVE, true) } else { DPAC_NX_SV(DPAC_SCHEME_NAIVE, false) }
+          if (gphase != DPAC_GUARD_FALLBACK_ONLY) {
+            if (adaptive) {
+              if (cost) { DPAC_NX_SV(DPAC_SCHEME_ADAPTIVE, true) } else { DPAC_NX_SV(DPAC_SCHEME_ADAPTIVE, false) }
+            } else {
+              if (cost) { DPAC_NX_SV(DPAC_SCHEME_NAIVE, true) } else { DPAC_NX_SV(DPAC_SCHEME_NAIVE, false) }
+            }
           }
 #undef DPAC_NX_SV
 #undef DPAC_NX_LAUNCH
           if (e != hipSuccess) return (int)e;
-          if (!m.status) break;
+          if (!m.status || gphase == DPAC_GUARD_SPLIT_ONLY) break;
           r.guard = m.status;  // then the f32 kernel below, run only once the x3 kernel fell back
         }
       }
+      if (gphase == DPAC_GUARD_FALLBACK_ONLY && !r.guard) break;  // phase 1 did the whole work
 #define DPAC_ROLL_NN(SCH, CO)                                                                                   \
   do {                                                                                                          \
     if (m.fast && r.save_mask)                                                                                  \

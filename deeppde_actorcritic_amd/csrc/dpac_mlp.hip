@@ -280,7 +280,8 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
         a.part = (float*)ws;
         a.status = net.status;
         const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
-        for (int l = 0; l <= a.L; ++l) {
+        const bool fb_only = net.guard_phase == DPAC_GUARD_FALLBACK_ONLY;
+        for (int l = 0; l <= a.L && !fb_only; ++l) {
           // a run of adjacent layers of the merged-group kernel's 13-tile bin (the wide hidden
           // layers, and the output layer after them): one launch (k_param_grads_x3w, lsel < 0)
           // (and the input layer before them, run by the same kernel at run time)
@@ -305,7 +306,8 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
           else e = launch_f32_layer<float>(a, l, nch, s0);
           if (e) return e;
         }
-        if (net.status) {  // the f32 kernel over every layer, run only once an x3 kernel fell back
+        if (net.status && net.guard_phase != DPAC_GUARD_SPLIT_ONLY) {
+          // the f32 kernel over every layer, run only once an x3 kernel fell back
           PgArgs<float> f = a;
           f.status = nullptr;
           f.guard = net.status;
@@ -318,13 +320,16 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
           if (hipError_t e = hipGetLastError()) return (int)e;
         }
         const int64_t n = a.ptot + a.width[a.L + 1];
+        PgArgs<float> r = a;  // phase 2: the reduce too runs only once an x3 kernel fell back
+        r.guard = fb_only ? net.status : nullptr;
         hipLaunchKernelGGL(k_param_grads_reduce<float>, dim3((unsigned)((n + kRedCols - 1) / kRedCols)), dim3(256), 0, s0,
-                           a, (int)nch, (float)gamma_scale, (float*)out);
+                           r, (int)nch, (float)gamma_scale, (float*)out);
         return (int)hipGetLastError();
       }
       a.rows_per_chunk = pg_chunk_rows<T>(rows, max_ld(a));
     }
   }
+  if (net.guard_phase == DPAC_GUARD_FALLBACK_ONLY) return 0;  // phase 1 did the whole work
   a.part = (T*)ws;
   const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
   // narrow layers (K or H <= 32: grids of 256-512 small workgroups) on the forked
@@ -468,15 +473,17 @@ int rows_fwd(int64_t rows, const dpac_mlp& net, const void* x, int64_t ldx, void
       xa.z = (float*)save_z;
       xa.status = net.status;
       xa.mask = (save_z && kX3RT == 4) ? reinterpret_cast<uint32_t*>(mask) : nullptr;  // 64-row blocks
-      if (int e = x3_launch(k_mlp_rows_fwd_x3, xa, s)) return e;
+      if (net.guard_phase != DPAC_GUARD_FALLBACK_ONLY)
+        if (int e = x3_launch(k_mlp_rows_fwd_x3, xa, s)) return e;
       if (written && xa.mask) *written = 1;
-      if (!net.status) return 0;
+      if (!net.status || net.guard_phase == DPAC_GUARD_SPLIT_ONLY) return 0;
       a.guard = net.status;  // the f32 kernel recomputes everything once the x3 kernel fell back
       hipLaunchKernelGGL(k_mlp_rows_fwd<T>, dim3((unsigned)std::min(nblk, kFallbackBlocks)), dim3(kMrThreads), 0,
                          s, a);
       return (int)hipGetLastError();
     }
   }
+  if (net.guard_phase == DPAC_GUARD_FALLBACK_ONLY) return 0;  // phase 1 did the whole work
   hipLaunchKernelGGL(k_mlp_rows_fwd<T>, dim3((unsigned)nblk), dim3(kMrThreads), 0, s, a);
   return (int)hipGetLastError();
 }
@@ -494,10 +501,11 @@ int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const voi
       a.g_x = (float*)g_x;
       a.status = net.status;
       a.mask = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(mask));
-      if (int e = mask ? x3_launch(k_mlp_rows_bwd_x3<true>, a, s, kX3RowsB, kX3LdsBytesB)
-                       : x3_launch(k_mlp_rows_bwd_x3<false>, a, s, kX3RowsB, kX3LdsBytesB))
-        return e;
-      if (!net.status) return 0;
+      if (net.guard_phase != DPAC_GUARD_FALLBACK_ONLY)
+        if (int e = mask ? x3_launch(k_mlp_rows_bwd_x3<true>, a, s, kX3RowsB, kX3LdsBytesB)
+                         : x3_launch(k_mlp_rows_bwd_x3<false>, a, s, kX3RowsB, kX3LdsBytesB))
+          return e;
+      if (!net.status || net.guard_phase == DPAC_GUARD_SPLIT_ONLY) return 0;
       MrArgs<T> f = mr_args<T>(net, rows);  // the f32 kernel, run only once the x3 kernel fell back
       set_td(f, td);
       if (td) f.g_gdot = (const T*)td->g_gdot;
@@ -513,6 +521,7 @@ int rows_bwd(int64_t rows, const dpac_mlp& net, const void* const* wt, const voi
       return (int)hipGetLastError();
     }
   }
+  if (net.guard_phase == DPAC_GUARD_FALLBACK_ONLY) return 0;  // phase 1 did the whole work
   MrArgs<T> a = mr_args<T>(net, rows);
   set_td(a, td);
   if (td) a.g_gdot = (const T*)td->g_gdot;

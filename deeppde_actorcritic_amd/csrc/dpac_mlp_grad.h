@@ -292,6 +292,8 @@ constexpr int kRedCols = 32, kRedSlices = 8;  // 256 threads
 template <typename T>
 __global__ __launch_bounds__(256) void k_param_grads_reduce(const PgArgs<T> a, int nchunks,
                                                             T gamma_scale, T* out) {
+  // a deferred fallback's reduce (dpac.h guard_phase 2): only once an x3 kernel fell back
+  if (a.guard && !x3_status_set(a.guard)) return;
   __shared__ T s_part[kRedSlices][kRedCols];
   const int col = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
   const int64_t p = (int64_t)blockIdx.x * kRedCols + col;

@@ -9,6 +9,7 @@ missing: there is no CPU path in the product.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -65,6 +66,8 @@ def sample(eqp, sample_type: int, num_sample: int, num_steps: int, seed: int,
     device = torch.device(device if device is not None else "cuda")
     if device.type != "cuda":
         raise _lib.DpacUnavailable("dpac_sample needs a GPU device")
+    if device.index is None:  # "cuda": the current device, as torch.empty places it
+        device = torch.device("cuda", torch.cuda.current_device())
     _lib.load()
     d = eqp.dim
     if out is not None:
@@ -159,6 +162,12 @@ class MlpView:
     def supported(self) -> bool:
         return max(self.widths) <= _lib.MLP_MAX_WIDTH
 
+    def phase_struct(self, phase: int):
+        """A copy of the struct with dpac_mlp.guard_phase = phase (dpac.h DPAC_GUARD_*)."""
+        m = _lib.Mlp.from_buffer_copy(self.struct)
+        m.guard_phase = phase
+        return m
+
     @property
     def scales(self):
         return self.tensors[:len(self.widths)]
@@ -202,6 +211,42 @@ def x3_fell_back(device="cuda") -> bool:
     """Whether a split-fp16 launch on `device` met an operand outside the split range (its
     launches, and every later one, then ran on the exact-f32 kernels).  Synchronises."""
     return bool(int(x3_status(device).item()) & _lib.X3_FELL_BACK)
+
+
+# Deferred range-guard fallbacks (dpac.h dpac_mlp.guard_phase, round 6).  Inside
+# deferred_fallbacks(sink) the guarded backward calls below (the actor's BPTT, the row backward
+# chains, the parameter gradients) launch only their split-fp16 kernels (phase 1) and append to
+# `sink` a callable that launches their guarded f32 fallbacks (phase 2) on the then-current
+# stream.  The caller runs the sink, in order, once every phase-1 call's inputs are final and
+# before any of their outputs is used: the solver captures it into one "redo" graph replayed
+# after the actor's and G's gradient chains have joined, so the no-op fallbacks no longer sit
+# between a chain's kernels waiting for CUs the other stream holds (VERDICT r05 item 2).  Only
+# chains whose outputs reach the caller with no torch op in between may be deferred: a phase-2
+# call rewrites its outputs, not what was computed from them.  The closures hold every tensor
+# the calls read or write, so a captured graph's pool cannot reuse them.
+_DEFER = None
+
+
+@contextlib.contextmanager
+def deferred_fallbacks(sink):
+    """Defer the guarded fallbacks of the calls inside into `sink` (a list); None: no deferral."""
+    global _DEFER
+    prev, _DEFER = _DEFER, sink
+    try:
+        yield sink
+    finally:
+        _DEFER = prev
+
+
+def _guarded_call(view: "MlpView", name: str, build):
+    """call(name, *build(ref to a dpac_mlp)) for a guarded entry point: inline (phase 0), or,
+    inside deferred_fallbacks, phase 1 now and phase 2 appended to the sink."""
+    if _DEFER is None or view.status is None:
+        call(name, *build(ctypes.byref(view.struct)))
+        return
+    s1, s2 = view.phase_struct(_lib.GUARD_SPLIT_ONLY), view.phase_struct(_lib.GUARD_FALLBACK_ONLY)
+    call(name, *build(ctypes.byref(s1)))
+    _DEFER.append(lambda: call(name, *build(ctypes.byref(s2))))
 
 
 def x3_status_reset(device="cuda") -> None:
@@ -467,9 +512,9 @@ def mlp_param_grads(view: "MlpView", x, z, G, like, ws_tag: int = 0):
     flat = torch.empty(total, dtype=x.dtype, device=x.device)
     if x.stride(1) != 1 or not z.is_contiguous() or not G.is_contiguous():
         raise ValueError("mlp_param_grads: x needs unit column stride, z and G contiguous")
-    call("dpac_mlp_param_grads", dt, R, ctypes.byref(view.struct), bn_rs_host(x.dtype),
-         ctypes.c_void_p(x.data_ptr()),
-         x.stride(0), _ptr(z), _ptr(G), _ptr(ws), ws.numel(), _ptr(flat), _stream(x))
+    _guarded_call(view, "dpac_mlp_param_grads", lambda v: (
+        dt, R, v, bn_rs_host(x.dtype), ctypes.c_void_p(x.data_ptr()), x.stride(0), _ptr(z), _ptr(G),
+        _ptr(ws), ws.numel(), _ptr(flat), _stream(x)))
     out, o = [], 0
     for p in like:
         out.append(flat[o:o + p.numel()].view(p.shape))
@@ -491,10 +536,10 @@ def _bptt_fused(eqp, scheme, T, N, L, x, u, dw, z, flag, disc_t, view, wt, wt_km
     B = x.shape[1]
     goff = np.cumsum([0] + widths).tolist()
     Gall = torch.empty(N, B, goff[-1], dtype=x.dtype, device=x.device)
-    call("dpac_rollout_nn_bwd_masked", ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T),
-         ctypes.byref(view.struct), _ptr_array(wt), _ptr_array(wt_km), _ptr(x), _ptr(u), _ptr(dw),
-         _ptr(z), _ptr(flag), _ptr(disc_t), _ptr(mask), _ptr(g_xN), _ptr(g_disc), _ptr(g_y), _ptr(Gall),
-         None, _stream(x))
+    _guarded_call(view, "dpac_rollout_nn_bwd_masked", lambda v: (
+        ctypes.byref(eqp), scheme, _dtype_id(x), B, N, float(T), v, _ptr_array(wt), _ptr_array(wt_km),
+        _ptr(x), _ptr(u), _ptr(dw), _ptr(z), _ptr(flag), _ptr(disc_t), _ptr(mask), _ptr(g_xN),
+        _ptr(g_disc), _ptr(g_y), _ptr(Gall), None, _stream(x)))
     return [Gall[:, :, goff[i]:goff[i + 1]] for i in range(L + 2)]
 
 
@@ -640,8 +685,10 @@ def row_mlp_backward(rs, params, x, z, g_out, want_x: bool, want_params: bool, w
     R = x.shape[0]
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
     g_x = torch.empty(R, view.widths[0], dtype=x.dtype, device=x.device) if want_x else None
-    call("dpac_mlp_rows_bwd_masked", _dtype_id(x), R, ctypes.byref(view.struct), _ptr_array(wt),
-         _ptr_array(wt_km), _ptr(z), _ptr(mask), _ptr(g_out.contiguous()), _ptr(G), _ptr(g_x), _stream(x))
+    g_out = g_out.contiguous()
+    _guarded_call(view, "dpac_mlp_rows_bwd_masked", lambda v: (
+        _dtype_id(x), R, v, _ptr_array(wt), _ptr_array(wt_km), _ptr(z), _ptr(mask), _ptr(g_out), _ptr(G),
+        _ptr(g_x), _stream(x)))
     grads = mlp_param_grads(view, x, z, G, params, ws_tag) if want_params else None
     return g_x, grads
 
@@ -732,10 +779,11 @@ def row_mlp_backward_td1(eqp, rs, params, x, z, u, dw, g_gdot, want_params: bool
     view, wt, wt_km = mlp_prepare(gam, bet, Ws, b, False, True)
     R = x.shape[0]
     G = torch.empty(R, sum(view.widths), dtype=x.dtype, device=x.device)
-    call("dpac_mlp_rows_bwd_td1_masked", ctypes.byref(eqp), _dtype_id(x), R, ctypes.byref(view.struct),
-         _ptr_array(wt), _ptr_array(wt_km), _ptr(z), _ptr(mask), ctypes.c_void_p(x.data_ptr()), x.stride(0),
-         _ptr(u.contiguous()), _ptr(dw.contiguous()), _ptr(g_gdot.contiguous()), _ptr(G), None,
-         _stream(x))
+    u, dw, g_gdot = u.contiguous(), dw.contiguous(), g_gdot.contiguous()
+    _guarded_call(view, "dpac_mlp_rows_bwd_td1_masked", lambda v: (
+        ctypes.byref(eqp), _dtype_id(x), R, v, _ptr_array(wt), _ptr_array(wt_km), _ptr(z), _ptr(mask),
+        ctypes.c_void_p(x.data_ptr()), x.stride(0), _ptr(u), _ptr(dw), _ptr(g_gdot), _ptr(G), None,
+        _stream(x)))
     return mlp_param_grads(view, x, z, G, params, ws_tag) if want_params else None
 
 

@@ -12,6 +12,8 @@ gradients and the critic's G half together (allreduce_grads_multi), SURVEY §8(e
 """
 from __future__ import annotations
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -33,6 +35,7 @@ class DataParallel:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.grad_allreduces = 0  # gradient all-reduces issued (tests count them per iteration)
+        self.timings = None  # a list: each gradient all-reduce appends (start, end event, host s)
 
     def shard(self, total: int):
         return shard_range(total, self.rank, self.world)
@@ -58,7 +61,15 @@ class DataParallel:
         if not pieces:
             return [list(grads) for grads, _, _ in parts]
         flat = torch.cat(pieces) if len(pieces) > 1 else pieces[0]
+        timed = self.timings is not None and flat.is_cuda
+        if timed:  # HIP events on the calling stream bracket the exchange (bench.py)
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            h0 = time.perf_counter()
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        if timed:
+            ev[1].record()
+            self.timings.append((ev[0], ev[1], time.perf_counter() - h0))
         self.grad_allreduces += 1
         outs, i = [], 0
         for grads, _, _ in parts:

@@ -17,6 +17,7 @@ Both give the same values and gradients.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 import time
@@ -340,6 +341,19 @@ class _GradGraph:
         return list(self.out)
 
 
+def _capture_redo(fns):
+    """The deferred range-guard fallbacks a capture collected (ops.deferred_fallbacks) as one
+    HIP graph, or None when there are none: no-op kernels while the split-fp16 status word
+    is clear, the exact-f32 recomputation of their chains once it is set."""
+    if not fns:
+        return None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+        for f in fns:
+            f()
+    return g
+
+
 class _SplitActorGraphs:
     """The actor step as two HIP graphs: the fused forward rollout with its backward
     saves (replayed on a side stream, so it runs beside the critic step: it reads only
@@ -348,19 +362,27 @@ class _SplitActorGraphs:
     solver.py:67-70 order).  The backward graph reads the forward graph's outputs in
     place: nothing is copied between them."""
 
-    def __init__(self, fwd_fn, bwd_fn, batch: TrajectoryBatch, side):
+    def __init__(self, fwd_fn, bwd_fn, batch: TrajectoryBatch, side, defer=None):
+        """defer: a context manager factory yielding the list the backward's deferred guard
+        fallbacks go to (ActorCriticSolver._deferring); they become the graph g_redo."""
         self.static = TrajectoryBatch(*[t.clone() for t in batch])
         self.side = side
+        defer = defer or (lambda: contextlib.nullcontext([]))
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up outside the capture (allocator, autograd)
             for _ in range(2):
-                bwd_fn(fwd_fn(self.static))
+                with defer() as fns:
+                    bwd_fn(fwd_fn(self.static))
+                for f in fns:
+                    f()
         torch.cuda.current_stream().wait_stream(side)
         self.g_fwd, self.g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fwd, capture_error_mode=_CAPTURE_MODE):
             self.fwd = fwd_fn(self.static)
         with torch.cuda.graph(self.g_bwd, capture_error_mode=_CAPTURE_MODE):
-            self.out = bwd_fn(self.fwd)
+            with defer() as self.redo_fns:
+                self.out = bwd_fn(self.fwd)
+        self.g_redo = _capture_redo(self.redo_fns)
 
     def launch_forward(self, batch: TrajectoryBatch):
         """On the side stream, after the work queued so far on the current stream."""
@@ -372,9 +394,15 @@ class _SplitActorGraphs:
             self.g_fwd.replay()
 
     def grads(self):
+        """The gradients (valid once redo() has run after them)."""
         torch.cuda.current_stream().wait_stream(self.side)
         self.g_bwd.replay()
         return list(self.out)
+
+    def redo(self):
+        """The backward's deferred guard fallbacks, on the current stream."""
+        if self.g_redo is not None:
+            self.g_redo.replay()
 
 
 class _SplitCriticGraphs:
@@ -387,15 +415,20 @@ class _SplitCriticGraphs:
     small kernels that leaves most CUs idle) and then beside the actor's BPTT, which needs
     the updated V only (solver.py:221), not G."""
 
-    def __init__(self, head_fn, v_fn, back_fn, batch: TrajectoryBatch, side):
+    def __init__(self, head_fn, v_fn, back_fn, batch: TrajectoryBatch, side, defer=None):
+        """defer: as _SplitActorGraphs's, for the G backward (graph g_redo)."""
         self.static = TrajectoryBatch(*[t.clone() for t in batch])
         self.side = side
+        defer = defer or (lambda: contextlib.nullcontext([]))
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):  # warm-up outside the capture (allocator, autograd)
             for _ in range(2):
                 h = head_fn(self.static)
                 v_fn(h[0])
-                back_fn((None,) + tuple(h[1]))
+                with defer() as fns:
+                    back_fn((None,) + tuple(h[1]))
+                for f in fns:
+                    f()
         torch.cuda.current_stream().wait_stream(side)
         self.g_head, self.g_v, self.g_back = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_head, capture_error_mode=_CAPTURE_MODE):
@@ -403,7 +436,9 @@ class _SplitCriticGraphs:
         with torch.cuda.graph(self.g_v, capture_error_mode=_CAPTURE_MODE):
             self.v_out = v_fn(self.head_out[0])
         with torch.cuda.graph(self.g_back, capture_error_mode=_CAPTURE_MODE):
-            self.back_out = back_fn((None,) + tuple(self.head_out[1]))
+            with defer() as self.redo_fns:
+                self.back_out = back_fn((None,) + tuple(self.head_out[1]))
+        self.g_redo = _capture_redo(self.redo_fns)
 
     def head(self, batch: TrajectoryBatch):
         """The head graph on the current stream."""
@@ -419,11 +454,17 @@ class _SplitCriticGraphs:
 
     def launch_back(self, after: torch.cuda.Event):
         """G's parameter gradients, replayed on the side stream once `after` (recorded
-        behind head()) has passed; use them on the side stream."""
+        behind head()) has passed; use them on the side stream (valid once redo() has run)."""
         self.side.wait_event(after)
         with torch.cuda.stream(self.side):
             self.g_back.replay()
         return list(self.back_out)
+
+    def redo(self):
+        """The G backward's deferred guard fallbacks, on the current stream (after it has
+        waited for the side stream)."""
+        if self.g_redo is not None:
+            self.g_redo.replay()
 
 
 # DPAC_GRAPH_SETS=2 (default): train_iteration alternates two sets of the split graphs and
@@ -432,6 +473,12 @@ class _SplitCriticGraphs:
 GRAPH_SETS = int(os.environ.get("DPAC_GRAPH_SETS", "2"))
 if GRAPH_SETS not in (1, 2):
     raise ValueError(f"DPAC_GRAPH_SETS must be 1 or 2, got {GRAPH_SETS}")
+
+# DPAC_GUARD_DEFER=1 (default): the split graphs' backward chains (the actor's BPTT and its
+# parameter gradients, G's row backward and parameter gradients) launch their range-guard
+# fallbacks not behind each split-fp16 launch but together, after the two chains have joined
+# (ops.deferred_fallbacks, dpac.h guard_phase; round 6); 0: inline, as before.
+GUARD_DEFER = os.environ.get("DPAC_GUARD_DEFER", "1") != "0"
 
 # DPAC_GBACK=late (default): the critic's G backward is launched on its side stream after V's
 # update and the actor's BPTT are queued, so it runs beside the BPTT and the actor's
@@ -532,6 +579,20 @@ class ActorCriticSolver(object):
         self._parity = 0          # the set the next train_iteration uses
         self._set_done = [None, None]  # event after the last iteration that used each set
         self._consts = {}  # constant operands of the graphs (never written)
+        self._redo_sink = None  # a list while a split graph's capture collects deferred fallbacks
+
+    @contextlib.contextmanager
+    def _deferring(self):
+        """Collect the guarded backward chains' deferred fallbacks (ops.deferred_fallbacks) of
+        the enclosed actor_grads_from / critic_G_back calls: yields the list."""
+        prev, self._redo_sink = self._redo_sink, []
+        try:
+            yield self._redo_sink
+        finally:
+            self._redo_sink = prev
+
+    def _defer(self):
+        return self._deferring if GUARD_DEFER else None
 
     # ---- variables ---------------------------------------------------------
     def critic_variables(self):
@@ -559,7 +620,11 @@ class ActorCriticSolver(object):
 
     def sample_iteration(self, num_sample, N_critic, N_actor):
         """The (critic, actor) samples of one training iteration (solver.py:67-70): the pair
-        prefetch_samples() drew on a side stream if it matches, else drawn now."""
+        prefetch_samples() drew on a side stream if it matches, else drawn now.
+
+        With GRAPH_SETS = 2 the prefetched pair IS the static input of a captured graph set:
+        the next prefetch_samples() into that set (two iterations later) overwrites it in
+        place.  A caller that keeps a batch beyond its train_iteration must clone it."""
         spec = (num_sample, N_critic, N_actor)
         nxt, self._next_samples = self._next_samples, None
         if nxt is None or nxt[0] != spec:
@@ -685,9 +750,10 @@ class ActorCriticSolver(object):
         g_xN = gV * (disc / B).unsqueeze(1)
         net = self.model_actor.NN_control
         ec = self.eqn_config
-        return ops.actor_bptt_grads(eqp, self.model_actor.scheme, ec.total_time_actor,
-                                    ec.num_time_interval_actor, net.ekn_head, net.bn_rs,
-                                    net.trainable_variables(), saved, g_y, g_disc, g_xN)
+        with ops.deferred_fallbacks(self._redo_sink):  # the BPTT -> parameter gradients chain
+            return ops.actor_bptt_grads(eqp, self.model_actor.scheme, ec.total_time_actor,
+                                        ec.num_time_interval_actor, net.ekn_head, net.bn_rs,
+                                        net.trainable_variables(), saved, g_y, g_disc, g_xN)
 
     # ---- the critic step split at the G network (its backward beside the BPTT) ----
     def _critic_split_ok(self):
@@ -760,7 +826,7 @@ class ActorCriticSolver(object):
         """G's parameter gradients from critic_front's outputs (dpac_mlp_rows_bwd[_td1] +
         dpac_mlp_param_grads, on their own scratch buffer: they run beside the BPTT)."""
         net = self.model_critic.NN_value_grad
-        with torch.no_grad():
+        with torch.no_grad(), ops.deferred_fallbacks(self._redo_sink):  # row backward -> gradients
             if len(front) == 7:  # fused TD1: dL/dG formed from dL/dgdot in the prologue
                 _, g_gdot, rows, z, m, u_rows, dw_rows = front
                 return ops.row_mlp_backward_td1(self.bsde.params(), net.bn_rs,
@@ -791,7 +857,7 @@ class ActorCriticSolver(object):
             sg = self._graphs.get(key)
             if sg is None:
                 sg = self._graphs[key] = _SplitActorGraphs(self.actor_forward, self.actor_grads_from,
-                                                           da, self._side)
+                                                           da, self._side, self._defer())
             sg.launch_forward(da)
             self.train_step_critic(data_critic, total)
             cg = None
@@ -803,9 +869,10 @@ class ActorCriticSolver(object):
             sets = self._gsets.setdefault(spec, [None, None])
             p = self._parity
             if sets[p] is None:
-                sets[p] = (_SplitActorGraphs(self.actor_forward, self.actor_grads_from, da, self._side),
+                sets[p] = (_SplitActorGraphs(self.actor_forward, self.actor_grads_from, da, self._side,
+                                             self._defer()),
                            _SplitCriticGraphs(self.critic_head, self.critic_grads_v, self.critic_G_back, dc,
-                                              self._side_g))
+                                              self._side_g, self._defer()))
             sg, cg = sets[p]
             sg.launch_forward(da)
             ccnt = dc.x0.shape[0]
@@ -824,12 +891,15 @@ class ActorCriticSolver(object):
         cnt = da.x0.shape[0]
         atot = total or cnt * self.par.world
         if cg is None:
+            sg.redo()
             g = self.par.allreduce_grads(g, cnt, atot)
             self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))
             return
         if GBACK != "early":
             gG = cg.launch_back(head_done)
         torch.cuda.current_stream().wait_stream(cg.side)  # G's gradients, made on the side stream
+        sg.redo()  # both chains' deferred range-guard fallbacks: no-ops unless a split operand overflowed
+        cg.redo()
         g, gG = self.par.allreduce_grads_multi([(g, cnt, atot), (gG, ccnt, ctot)])
         self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))
         self.optimizer_critic.apply_gradients(zip(gG, self.model_critic.NN_value_grad.trainable_variables()))

@@ -55,9 +55,10 @@ extern "C" {
  * (below) and the float fused rollout / BPTT (dpac_rollout_nn_fwd[_masked],
  * dpac_rollout_nn_bwd_masked) read them too.  5: adds dpac_critic_loss_grad.  6: dpac_mlp gains
  * `status` (the split-fp16 range guard, below).  7: adds the row kernels' sign-bit mask
- * (dpac_mlp_rows_mask_bytes, dpac_mlp_rows_{fwd,bwd}[_td1]_masked).  Bindings must refuse a
- * library of another version. */
-#define DPAC_ABI_VERSION 7
+ * (dpac_mlp_rows_mask_bytes, dpac_mlp_rows_{fwd,bwd}[_td1]_masked).  8: dpac_mlp gains
+ * `guard_phase` (the range guard's fallback launched apart from its split-fp16 launch, below).
+ * Bindings must refuse a library of another version. */
+#define DPAC_ABI_VERSION 8
 
 /* status codes besides hipError_t values */
 #define DPAC_OK 0
@@ -282,6 +283,18 @@ int dpac_actor_cost_fwd(const dpac_eqn_params* eq, int32_t dtype,
  *     The f32 fallback needs the f32 operands of the direction: weight and weight_km (forward
  *     entry points), weight_t and weight_t_km (backward entry points); without them the
  *     split-fp16 kernels are not used when a status word is given.
+ *   guard_phase (with a status word; 0 when no status is given): which launches of a guarded
+ *     call are made.  DPAC_GUARD_INLINE (0): the split-fp16 launch and then its guarded f32
+ *     fallback, as above.  DPAC_GUARD_SPLIT_ONLY (1): the split-fp16 launch (and the launches
+ *     that follow it unconditionally, e.g. the parameter gradients' reduce) but not the fallback.
+ *     DPAC_GUARD_FALLBACK_ONLY (2): only the guarded fallback of the same call (and, for the
+ *     parameter gradients, a guarded reduce after it): no-ops while the word is clear, and with
+ *     the word set they rewrite every output from the call's inputs.  A caller may therefore
+ *     make a chain of phase-1 calls and their phase-2 calls later, in the same order on one
+ *     stream, as long as the inputs of every call stay unchanged until its phase-2 call (a
+ *     split-fp16 launch that finds the word set does no work, so every phase-2 call after it
+ *     recomputes the chain).  Calls whose launches do not use the split-fp16 kernels make their
+ *     whole work in phase 1 and nothing in phase 2.
  * 1 <= n_hidden <= DPAC_MLP_MAX_HIDDEN, every width <= DPAC_MLP_MAX_WIDTH.
  * Outputs as dpac_rollout_fwd, with u [N][B][c] the control actually applied.
  * y/disc (optional, both or neither): the pathwise cost in `cost_order`.
@@ -303,8 +316,12 @@ typedef struct dpac_mlp {
   const void* weight_x3[DPAC_MLP_MAX_HIDDEN + 1];
   const void* weight_t_x3[DPAC_MLP_MAX_HIDDEN + 1];
   uint32_t* status; /* the split-fp16 range guard (above); NULL = unguarded */
+  int32_t guard_phase; /* DPAC_GUARD_* (above); 0 = the split-fp16 launch and its fallback */
 } dpac_mlp;
 #define DPAC_X3_FELL_BACK 1u /* status bit: an operand left the split-fp16 range */
+#define DPAC_GUARD_INLINE 0
+#define DPAC_GUARD_SPLIT_ONLY 1
+#define DPAC_GUARD_FALLBACK_ONLY 2
 
 int dpac_rollout_nn_fwd(const dpac_eqn_params* eq, int32_t scheme, int32_t dtype,
                         int64_t num_sample, int32_t num_steps, double total_time,

@@ -53,7 +53,9 @@ def test_constants_match_header():
              "DPAC_SAMPLE_NORMAL": _lib.SAMPLE_NORMAL, "DPAC_SAMPLE_BOUNDED": _lib.SAMPLE_BOUNDED,
              "DPAC_SAMPLE_ZERO_X0": _lib.SAMPLE_ZERO_X0, "DPAC_EVAL_B": _lib.EVAL_B,
              "DPAC_EVAL_V_GRAD": _lib.EVAL_V_GRAD, "DPAC_EINVAL": _lib.DPAC_EINVAL,
-             "DPAC_EUNSUP": _lib.DPAC_EUNSUP, "DPAC_X3_FELL_BACK": _lib.X3_FELL_BACK}
+             "DPAC_EUNSUP": _lib.DPAC_EUNSUP, "DPAC_X3_FELL_BACK": _lib.X3_FELL_BACK,
+             "DPAC_GUARD_INLINE": _lib.GUARD_INLINE, "DPAC_GUARD_SPLIT_ONLY": _lib.GUARD_SPLIT_ONLY,
+             "DPAC_GUARD_FALLBACK_ONLY": _lib.GUARD_FALLBACK_ONLY}
     for k, v in pairs.items():
         assert d[k] == v, k
 

@@ -63,4 +63,16 @@ def test_bench_gpus_2_gloo_rehearsal_reports_two_ranks():
     assert out["dist"]["world"] == 2 and out["dist"]["backend"] == "gloo"
     assert out["dist"]["launcher"] == "torch.distributed.run"
     assert out["value"] > 0 and out["roofline"]["frac"] > 0
-    print("gloo rehearsal line:", json.dumps({k: out[k] for k in ("value", "n_gpus", "ms_per_step")}))
+    assert out["dist"]["note"].startswith("ranks share a GPU")
+    # strong scaling: the global batch stays 4096, split 2048 + 2048
+    st = out["strong_scaling"]
+    assert st["scaling"] == "strong" and st["global_batch"] == 4096
+    assert st["batch_per_gpu"] == 2048 and st["batch_per_rank"] == [2048, 2048]
+    assert st["value"] > 0 and st["ms_per_step"] > 0 and 0 < st["roofline"]["frac"] < 1
+    assert st["roofline"]["peak"] == 2 * 8000.0
+    sp = out["speedup_vs_1"]
+    assert sp["one_gpu_value"] > 0
+    assert abs(sp["weak"] - out["value"] / sp["one_gpu_value"]) < 1e-9 * sp["weak"]
+    assert abs(sp["strong"] - st["value"] / sp["one_gpu_value"]) < 1e-9 * sp["strong"]
+    print("gloo rehearsal line:", json.dumps({k: out[k] for k in ("value", "n_gpus", "ms_per_step",
+                                                                  "speedup_vs_1")}))

@@ -172,3 +172,59 @@ def test_gback_early_and_late_give_bitwise_equal_parameters(monkeypatch):
         out[mode] = [v.detach().cpu().clone() for v in sp.critic_variables() + sp.actor_variables()]
     for a, b in zip(out["early"], out["late"]):
         assert torch.equal(a, b)
+
+
+def _production_params(monkeypatch, attr, value, iters=4, big=None):
+    """The float32 production path (HIP graphs, split steps, device sampler, lqr_d20 at B = 2048)
+    with psol.<attr> = value: the parameters after `iters` iterations of the loop solver.train
+    and bench.py run (sample_iteration / train_iteration / prefetch_samples).  big: every
+    network's first hidden BN scale times this factor (split-fp16 operands out of range)."""
+    from deeppde_actorcritic_amd import ops
+    from deeppde_actorcritic_amd.config import baseline_config
+    monkeypatch.setattr(psol, attr, value)
+    ops.x3_status_reset("cuda")
+    cfg = baseline_config(iters, 10 ** 9, "float32", 2048, 256, "lqr_d20")
+    sp = psol.ActorCriticSolver(cfg, peq.LQR(cfg.eqn_config), seed=5, sampler="device")
+    if big:
+        with torch.no_grad():
+            for net in (sp.model_critic.NN_value, sp.model_critic.NN_value_grad, sp.model_actor.NN_control):
+                net.bn_gamma[1].mul_(big)
+    for _ in range(iters):
+        dc, da = sp.sample_iteration(2048, 100, 100)
+        sp.train_iteration(dc, da, 2048)
+        sp.prefetch_samples(2048, 100, 100)
+    torch.cuda.synchronize()
+    assert sp._critic_split_ok()
+    fell = ops.x3_fell_back("cuda")
+    ops.x3_status_reset("cuda")
+    return [v.detach().cpu().clone() for v in sp.critic_variables() + sp.actor_variables()], fell
+
+
+def _bitwise(a, b):
+    torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+
+
+def test_graph_sets_one_and_two_give_bitwise_equal_parameters(monkeypatch):
+    """DPAC_GRAPH_SETS=2 (prefetch_samples draws the next iteration's samples on a
+    side stream straight into the idle graph set's static inputs, guarded by the event recorded
+    after the last iteration that used the set) against 1 (one set, the samples copied in):
+    bitwise the same parameters over 4 iterations, so no reader of a set's inputs (the side
+    stream's forward replay, the G backward's dw rows) races the next draw."""
+    p1, _ = _production_params(monkeypatch, "GRAPH_SETS", 1)
+    p2, _ = _production_params(monkeypatch, "GRAPH_SETS", 2)
+    for a, b in zip(p1, p2):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("big", [None, 2.0 ** 20])
+def test_guard_deferred_and_inline_give_bitwise_equal_parameters(monkeypatch, big):
+    """Round 6: the backward chains' range-guard fallbacks replayed as one
+    redo graph after the actor's and G's chains join (DPAC_GUARD_DEFER=1, the default) against
+    each fallback right behind its split-fp16 launch (0): bitwise the same parameters over 4
+    iterations, in range (the fallbacks stay no-ops) and with every network's BN_1 times 2^20
+    (the status word is set and the deferred fallbacks recompute the chains in exact f32)."""
+    pi, fi = _production_params(monkeypatch, "GUARD_DEFER", False, big=big)
+    pd, fd = _production_params(monkeypatch, "GUARD_DEFER", True, big=big)
+    assert fi == fd == (big is not None)
+    for a, b in zip(pi, pd):
+        _bitwise(a, b)

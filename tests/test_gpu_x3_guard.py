@@ -224,3 +224,85 @@ def test_fp32_production_gradients_with_out_of_range_networks_vs_oracle():
     ec, ea = _grad_err(gp_c, go_c), _grad_err(gp_a, go_a)
     print(f"\n[x3 guard, fp32 production vs oracle, BN_1 x 2^20] critic {ec:.2e}, actor {ea:.2e}")
     assert ec <= TOL_GRAD and ea <= TOL_GRAD
+
+
+def _bptt_and_grads(net, eqp, x0, dw, T, N, sink=None):
+    """_rollout_and_bptt's backward half (BPTT chain G + parameter gradients) with the forward
+    done inline; sink: a list, the backward calls' guard fallbacks deferred into it
+    (ops.deferred_fallbacks, dpac.h guard_phase)."""
+    view = net.mlp_view()
+    x, dt, coef, u, y, disc, saves = ops.rollout_nn(eqp, _lib.SCHEME_ADAPTIVE, x0, dw, T, N, view,
+                                                    cost_order=_lib.COST_ACTOR, save=True)
+    z, flag, disc_t, mask = saves
+    B = x0.shape[0]
+    gy = torch.full((B,), 1.0 / B, device=DEV)
+    gd = torch.randn(B, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1)) / B
+    gx = torch.randn(B, 20, device=DEV, generator=torch.Generator(device=DEV).manual_seed(2)) / B
+    params = [p.detach() for p in net.trainable_variables()]
+    with ops.deferred_fallbacks(sink):
+        grads = ops.actor_bptt_grads(eqp, _lib.SCHEME_ADAPTIVE, T, N, net.ekn_head, net.bn_rs, params,
+                                     (x, u, dw, z, flag, disc_t, mask), gy, gd, gx)
+    return grads
+
+
+@pytest.mark.parametrize("big", [None, 2.0 ** 20])
+def test_deferred_fallbacks_equal_inline_bitwise(big):
+    """dpac.h guard_phase (round 6): the actor's BPTT and parameter gradients
+    with their guard fallbacks deferred (phase 1 now, phase 2 later, in order) give bitwise the
+    gradients of the inline guard, in range (the fallbacks stay no-ops) and with BN_1 times 2^20
+    (the word is set by the forward: the phase-1 launches do nothing and the deferred fallbacks
+    recompute everything) — and out of range, the deferred phase is what fixes them."""
+    cfg = full_config("LQR", 20, N=16, hidden=(200, 200, 200), dtype="float32")
+    eqp = peq.LQR(cfg.eqn_config).params()
+    net = _net("actor", 1 if big else None, big=big or 1.0)
+    B, N, T = 2048, 16, 0.2
+    x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=9, dtype=torch.float32, device=DEV)
+    ref = [g.clone() for g in _bptt_and_grads(net, eqp, x0, dw, T, N)]
+    torch.cuda.synchronize()
+    assert ops.x3_fell_back(DEV) == (big is not None)
+    ops.x3_status_reset(DEV)
+    sink = []
+    got = _bptt_and_grads(net, eqp, x0, dw, T, N, sink)
+    assert len(sink) == 2  # the BPTT's and the parameter gradients' phase-2 calls
+    if big:  # the phase-1 launches did nothing: with the partial sums poisoned, the gradients
+        for ws in ops._WS_CACHE.values():  # are NaN until the deferred fallbacks run
+            ws.fill_(255)
+        got = _bptt_and_grads(net, eqp, x0, dw, T, N, [])  # (its own sink is dropped)
+        torch.cuda.synchronize()
+        assert not _finite(got)
+        ops.x3_status_reset(DEV)
+        sink = []
+        got = _bptt_and_grads(net, eqp, x0, dw, T, N, sink)
+    for f in sink:
+        f()
+    torch.cuda.synchronize()
+    assert ops.x3_fell_back(DEV) == (big is not None)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
+def test_deferred_row_backward_fallback_equals_inline_bitwise():
+    """The same for the row backward chain + parameter gradients (the critic's G network,
+    ops.row_mlp_backward) with BN_1 times 2^17."""
+    net = _net("critic_grad", 1)
+    R = 8192
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(R, 20, generator=gen, device=DEV)
+    g_out = torch.randn(R, 20, generator=gen, device=DEV) / R
+    params = [p.detach() for p in net.trainable_variables()]
+
+    def run(sink):
+        prep = net.mlp_prepared()
+        _, z = ops.mlp_rows(prep[0], x, save=True)
+        with ops.deferred_fallbacks(sink):
+            return ops.row_mlp_backward(net.bn_rs, params, x, z, g_out, True, True, prepared=prep)
+    gx_ref, g_ref = run(None)
+    ops.x3_status_reset(DEV)
+    sink = []
+    gx, g = run(sink)
+    assert len(sink) == 2
+    for f in sink:
+        f()
+    torch.cuda.synchronize()
+    assert ops.x3_fell_back(DEV)
+    assert torch.equal(gx, gx_ref) and all(torch.equal(a, b) for a, b in zip(g, g_ref))
