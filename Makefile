@@ -27,7 +27,7 @@ EQN_OBJS  := $(foreach e,$(EQNS),$(foreach d,$(call eqn_dims,$(e)),$(foreach t,f
 OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_params.o $(EQN_OBJS)
 LIB       := $(PKG)/libdpac.so
 
-.PHONY: all lib ext clean
+.PHONY: all lib ext bounds clean
 all: lib
 lib: $(LIB)
 
@@ -114,3 +114,16 @@ $(ASAN_DIR)/abi_sanitize: tests/abi_sanitize.c $(ASAN_DIR)/libdpac_asan.so inclu
 sanitize: $(ASAN_DIR)/abi_sanitize
 	ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
 	  $(ASAN_DIR)/abi_sanitize > $(ASAN_DIR)/abi_sanitize.log 2>&1; rc=$$?; tail -3 $(ASAN_DIR)/abi_sanitize.log; exit $$rc
+
+# The DPAC_CHECK_BOUNDS test build (dpac_device.h): the row kernels' object (dpac_mlp.hip) rebuilt
+# with every row-indexed TD-operand / prologue load checking that its row is live, linked with the
+# main build's other objects -> tools/variants/libdpac_bounds.so (DPAC_LIB=...;
+# tests/test_gpu_td_fused.py runs tests/bounds_check.py under it).
+BOUNDS_LIB := tools/variants/libdpac_bounds.so
+bounds: $(BOUNDS_LIB)
+build/bounds/dpac_mlp.o: $(CSRC)/dpac_mlp.hip $(OBJDIR)/dpac_mlp.o
+	@mkdir -p build/bounds
+	$(HIPCC) $(HIPFLAGS) -DDPAC_CHECK_BOUNDS=1 -c $< -o $@
+$(BOUNDS_LIB): build/bounds/dpac_mlp.o $(OBJS)
+	@mkdir -p tools/variants
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(filter-out $(OBJDIR)/dpac_mlp.o,$(OBJS)) build/bounds/dpac_mlp.o

@@ -153,6 +153,9 @@ def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total
     from deeppde_actorcritic_amd.config import baseline_config
     Bg = total or B
     progress(f"training variant {name}: batch {Bg} ({B} per rank)")
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    mem0 = torch.cuda.memory_allocated()
     cfg = baseline_config(iters, 10 ** 9, "float32" if dtype == torch.float32 else "float64", Bg, Bg, name=name)
     bsde = getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config)
     sp = psol.ActorCriticSolver(cfg, bsde, seed=1, sampler="device", parallel=par)
@@ -196,7 +199,10 @@ def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total
             "mlp": "20-200-200-200-%d" % cfg.eqn_config.control_dim, "ms_per_iteration": ms,
             "traj_steps_per_s": 2 * Bg * N / (ms * 1e-3),
             "mlp_executed_TFLOPs": 7 * rate, "mlp_reference_equiv_TFLOPs": 11 * rate,
-            "mlp_math": ops_mlp_math(dtype), "collectives": coll}
+            "mlp_math": ops_mlp_math(dtype), "collectives": coll, "graph_sets": psol.GRAPH_SETS,
+            "peak_memory_GB": (torch.cuda.max_memory_allocated() - mem0) / 1e9,
+            "peak_memory_note": "device memory this variant's solver, samples and HIP graph pools held at "
+                                "their peak, above what was allocated before it (torch caching allocator)"}
 
 
 def ops_mlp_math(dtype):

@@ -198,52 +198,66 @@ int launch(const OpArgs& a) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int N, int D, int sample_type,
                                                    uint64_t seed, int64_t traj_offset, T* dw) {
-  // one thread per (t, b, lane slot p, block): the stream layout of draw_slot()
+  // one thread per (unit u, b, lane slot p, block): the stream layout of draw_slot(); a unit is
+  // a step pair in the paired layout (S = 2), else one step
   const int P = lanes_for_dim(D), M = comps_per_lane(D);
-  const int PB = sample_type == DPAC_SAMPLE_BOUNDED ? 4 : Rng<T>::kNormalPerBlock;
-  const int BPL = (M + PB - 1) / PB;
-  const int64_t per_row = (int64_t)P * BPL;  // counter blocks per (t, b)
-  const int64_t total = (int64_t)N * B * per_row;
+  const int PB = dw_per_block<T>(sample_type);
+  const int S = dw_steps_per_block<T>(M, sample_type);
+  const int BPU = S == 2 ? 1 : (M + PB - 1) / PB;  // counter blocks per (unit, lane slot)
+  const int64_t units = S == 2 ? (N + 1) / 2 : N;
+  const int PL = (D + M - 1) / M;  // lane slots that own components (d = 20: 10 of P = 16)
+  (void)P;
+  const int64_t per_row = (int64_t)PL * BPU;  // counter blocks per (unit, b)
+  const int64_t total = units * B * per_row;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t tb = i / per_row;
-    const int rem = (int)(i - tb * per_row);
-    const int p = rem / BPL, blk = rem % BPL;
-    const int t = (int)(tb / B);
-    const int64_t b = tb - (int64_t)t * B;
+    const int64_t ub = i / per_row;
+    const int rem = (int)(i - ub * per_row);
+    const int p = rem / BPU, blk = rem % BPU;
+    const int u = (int)(ub / B);
+    const int64_t b = ub - (int64_t)u * B;
     const uint64_t traj = (uint64_t)(traj_offset + b);
-    const uint64_t block = (kTagDw << 48) | (((uint64_t)t * P + p) * BPL + blk);
-    const uint4 v = philox_block(seed, traj, block);
     T vals[4];
-    if (sample_type == DPAC_SAMPLE_BOUNDED) {
-      vals[0] = bounded_value<T>(v.x); vals[1] = bounded_value<T>(v.y);
-      vals[2] = bounded_value<T>(v.z); vals[3] = bounded_value<T>(v.w);
-    } else {
-      T n[Rng<T>::kNormalPerBlock];
-      Rng<T>::normals(v, n);
-#pragma unroll
-      for (int e = 0; e < Rng<T>::kNormalPerBlock; ++e) vals[e] = n[e];
-    }
-    T* out = dw + tb * D;
+    dw_block_values<T>(seed, traj, ((uint64_t)u * lanes_for_dim(D) + p) * BPU + blk, sample_type, vals);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int m = blk * PB + e, j = p * M + m;
-      if (e < PB && m < M && j < D) out[j] = vals[e];
+      if (e >= PB) break;
+      const int idx = blk * PB + e;  // the value's place in the lane slot's unit
+      const int t = S == 2 ? 2 * u + idx / M : u;
+      const int m = S == 2 ? idx % M : idx;
+      const int j = p * M + m;
+      if ((S == 2 ? idx < 2 * M : m < M) && t < N && j < D) dw[((int64_t)t * B + b) * D + j] = vals[e];
     }
   }
 }
 
-// Gaussian direction (tag) for component j of trajectory traj
+// A Gaussian direction (tag) of trajectory traj: component j is element j % PB of counter block
+// (tag << 48) | (j / PB).  dir_sumsq: sum_j g_j^2 in component order; dir_write: out[j] =
+// (scale * g_j) / nrm.  Each computes the ceil(D / PB) blocks once (round 6; rounds 1-5 drew a
+// whole block per component, twice).
 template <typename T>
-__device__ T dir_normal(uint64_t seed, uint64_t traj, uint64_t tag, int j) {
+__device__ T dir_sumsq(uint64_t seed, uint64_t traj, uint64_t tag, int D) {
   constexpr int PB = Rng<T>::kNormalPerBlock;
-  T n[PB];
-  Rng<T>::normals(philox_block(seed, traj, (tag << 48) | (uint64_t)(j / PB)), n);
-  const int e = j % PB;
-  T v = n[0];
+  T ss = 0;
+  for (int c = 0; c * PB < D; ++c) {
+    T n[PB];
+    Rng<T>::normals(philox_block(seed, traj, (tag << 48) | (uint64_t)c), n);
 #pragma unroll
-  for (int i = 1; i < PB; ++i) v = e == i ? n[i] : v;
-  return v;
+    for (int e = 0; e < PB; ++e)
+      if (c * PB + e < D) ss += n[e] * n[e];
+  }
+  return ss;
+}
+template <typename T>
+__device__ void dir_write(uint64_t seed, uint64_t traj, uint64_t tag, int D, T scale, T nrm, T* out) {
+  constexpr int PB = Rng<T>::kNormalPerBlock;
+  for (int c = 0; c * PB < D; ++c) {
+    T n[PB];
+    Rng<T>::normals(philox_block(seed, traj, (tag << 48) | (uint64_t)c), n);
+#pragma unroll
+    for (int e = 0; e < PB; ++e)
+      if (c * PB + e < D) out[c * PB + e] = (scale * n[e]) / nrm;
+  }
 }
 
 template <typename T>
@@ -264,24 +278,11 @@ __global__ __launch_bounds__(256) void k_sample_points(int64_t B, int D, double 
       if constexpr (sizeof(T) == 4) U = rocrand_device::detail::uniform_distribution(v.x);
       else U = rocrand_device::detail::uniform_distribution_double(v.x, v.y);
       const T r = pow(Rt * U, (T)1 / (T)D) * pow(Rt, (T)(D - 1) / (T)D);
-      T ss = 0;
-      for (int j = 0; j < D; ++j) {
-        const T g = dir_normal<T>(seed, traj, kTagDir, j);
-        ss += g * g;
-      }
-      const T nrm = sqrt(ss);
-      for (int j = 0; j < D; ++j) x0[b * D + j] = (r * dir_normal<T>(seed, traj, kTagDir, j)) / nrm;
+      dir_write<T>(seed, traj, kTagDir, D, r, sqrt(dir_sumsq<T>(seed, traj, kTagDir, D)), x0 + b * D);
     }
   }
-  if (x_bdry) {  // R * g / |g|  (:20-22)
-    T ss = 0;
-    for (int j = 0; j < D; ++j) {
-      const T g = dir_normal<T>(seed, traj, kTagBdry, j);
-      ss += g * g;
-    }
-    const T nrm = sqrt(ss);
-    for (int j = 0; j < D; ++j) x_bdry[b * D + j] = (Rt * dir_normal<T>(seed, traj, kTagBdry, j)) / nrm;
-  }
+  if (x_bdry)  // R * g / |g|  (:20-22)
+    dir_write<T>(seed, traj, kTagBdry, D, Rt, sqrt(dir_sumsq<T>(seed, traj, kTagBdry, D)), x_bdry + b * D);
 }
 
 template <typename T>
@@ -290,10 +291,12 @@ int sample_impl(const dpac_eqn_params* eq, int32_t sample_type, int64_t B, int32
   const int D = eq->dim;
   if (dw) {
     const int P = lanes_for_dim(D), M = comps_per_lane(D);
-    const int PB = sample_type == DPAC_SAMPLE_BOUNDED ? 4 : Rng<T>::kNormalPerBlock;
-    const int64_t total = (int64_t)N * B * P * ((M + PB - 1) / PB);
-    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
     const int st = sample_type == DPAC_SAMPLE_ZERO_X0 ? DPAC_SAMPLE_NORMAL : sample_type;
+    const int PB = dw_per_block<T>(st), S = dw_steps_per_block<T>(M, st);
+    const int PL = (D + M - 1) / M;  // lane slots that own components
+    (void)P;
+    const int64_t total = (S == 2 ? ((int64_t)N + 1) / 2 : (int64_t)N) * B * PL * (S == 2 ? 1 : (M + PB - 1) / PB);
+    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
     hipLaunchKernelGGL(k_sample_dw<T>, dim3((unsigned)blocks), dim3(256), 0, s, B, N, D, st, seed,
                        off, (T*)dw);
     if (hipError_t e = hipGetLastError()) return (int)e;

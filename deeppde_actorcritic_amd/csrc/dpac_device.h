@@ -172,6 +172,41 @@ __device__ __forceinline__ void buf_store_dwords(__amdgpu_buffer_rsrc_t r, uint3
 }
 
 template <typename T>
+__device__ __forceinline__ T buf_load_elem(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  uint32_t w[sizeof(T) / 4];
+  buf_load_dwords<sizeof(T) / 4>(r, voff, w);
+  T v;
+  __builtin_memcpy(&v, &w[0], sizeof(T));
+  return v;
+}
+
+// Rows [row0, row0 + live) of a [rows][ld] array as a buffer descriptor (round 6, VERDICT r05
+// item 6): element (r, k) sits at byte offset ((r - row0) ld + k) sizeof(T), and a row outside
+// the range reads 0 (a store to it is dropped) instead of reaching memory past the array.
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const T* base, int64_t row0, int live, int64_t ld) {
+  const bool any = base != nullptr && live > 0;
+  return make_rsrc(any ? base + row0 * ld : nullptr, any ? (uint32_t)((int64_t)live * ld * (int64_t)sizeof(T)) : 0u);
+}
+
+// DPAC_CHECK_BOUNDS=1 (a test build, `make bounds`): every row-indexed load of the row kernels'
+// TD operands and prologues checks that its row is live; a violation prints one line per wave
+// and reads 0 (the descriptors' behaviour), so a test run reports it without faulting the GPU.
+#ifndef DPAC_CHECK_BOUNDS
+#define DPAC_CHECK_BOUNDS 0
+#endif
+#if DPAC_CHECK_BOUNDS
+#define DPAC_CHECK_ROW(off, live)                                                                  \
+  do {                                                                                             \
+    if (!((int64_t)(off) >= 0 && (int64_t)(off) < (int64_t)(live)))                                \
+      printf("dpac bounds violation: row offset %lld of %d live rows at %s:%d\n",                 \
+             (long long)(off), (int)(live), __FILE__, __LINE__);                                   \
+  } while (0)
+#else
+#define DPAC_CHECK_ROW(off, live) ((void)0)
+#endif
+
+template <typename T>
 __device__ __forceinline__ void buf_store_scalar(__amdgpu_buffer_rsrc_t r, uint32_t voff, T v,
                                                  uint32_t soff = 0) {
   uint32_t w[sizeof(T) / 4];
@@ -319,12 +354,17 @@ struct Lanes {
 
 // ---------------------------------------------------------------------------
 // Brownian increments: rocRAND Philox4x32-10, subsequence = global trajectory
-// index g, key = seed.  With P = lanes_for_dim(d), M = comps_per_lane(d),
-// component j = p*M + m of step t is element (m % PB) of counter block
-// (tag << 48) | ((t*P + p)*BPL + m / PB), BPL = ceil(M / PB), where PB numbers
-// come out of one block: 4 float normals, 2 double normals, or 4 bounded values.
-// A lane draws exactly the components it owns, and the stream is a fixed
-// function of (seed, g, t, j) for every GPU count and batch split.
+// index g, key = seed.  With P = lanes_for_dim(d), M = comps_per_lane(d) and PB the
+// values one counter block yields (4 float normals, 2 double normals, 4 bounded values):
+//  * paired layout, when 2M <= PB (round 6; e.g. float at d = 20: M = 2, PB = 4): lane slot
+//    p draws the increments of TWO steps from one block, (tag << 48) | ((t/2)*P + p); value
+//    (t % 2)*M + m of the block is component j = p*M + m of step t.  Every value drawn is
+//    used (rounds 1-5 drew a block per step and kept M of its PB values);
+//  * otherwise (2M > PB: float64 normals at M >= 2, VDP's one-lane groups): component
+//    j = p*M + m of step t is element (m % PB) of block (tag << 48) | ((t*P + p)*BPL + m/PB),
+//    BPL = ceil(M / PB).
+// A lane draws exactly the components it owns, and the stream is a fixed function of
+// (seed, g, t, j) for every GPU count and batch split.
 // Normal: rocRAND's Box–Muller (float: box_muller_hw below; double:
 // normal_distribution_double2).  Bounded: k = floor(6·u32 / 2^32) ∈ {0..5},
 // value floor((k-1)/4)·√3 (equation.py:31-32).
@@ -382,11 +422,57 @@ __host__ __device__ constexpr int dw_per_block(int sample_type) {
   return sample_type == DPAC_SAMPLE_BOUNDED ? 4 : (sizeof(T) == 4 ? 4 : 2);
 }
 
+// Steps whose increments a lane slot draws from one counter block (the layout above): 2 when
+// both steps' M values fit one block, else 1.
+template <typename T>
+__host__ __device__ constexpr int dw_steps_per_block(int M, int sample_type) {
+  return 2 * M <= dw_per_block<T>(sample_type) ? 2 : 1;
+}
+
+// The values of one counter block of the dw stream (PB of them; the rest unset).
+template <typename T>
+__device__ __forceinline__ void dw_block_values(uint64_t seed, uint64_t traj, uint64_t block,
+                                                int sample_type, T (&v)[4]) {
+  const uint4 w = philox_block(seed, traj, (kTagDw << 48) | block);
+  if (sample_type == DPAC_SAMPLE_BOUNDED) {
+    v[0] = bounded_value<T>(w.x); v[1] = bounded_value<T>(w.y);
+    v[2] = bounded_value<T>(w.z); v[3] = bounded_value<T>(w.w);
+  } else {
+    T n[Rng<T>::kNormalPerBlock];
+    Rng<T>::normals(w, n);
+#pragma unroll
+    for (int e = 0; e < Rng<T>::kNormalPerBlock; ++e) v[e] = n[e];
+  }
+}
+
+// Paired layout (dw_steps_per_block == 2): lane slot p's increments of steps 2q (out[0 .. M))
+// and 2q + 1 (out[M .. 2M)), one counter block.
+template <typename T, int D>
+__device__ __forceinline__ void draw_slot_pair(uint64_t seed, uint64_t traj, int q, int p, int sample_type,
+                                               T (&out)[2 * comps_per_lane(D)]) {
+  constexpr int P = lanes_for_dim(D), M = comps_per_lane(D);
+  static_assert(2 * M <= 4, "a block holds at most 4 values");
+  T v[4];
+  dw_block_values<T>(seed, traj, (uint64_t)q * P + p, sample_type, v);
+#pragma unroll
+  for (int i = 0; i < 2 * M; ++i) out[i] = v[i];
+}
+
 // The M increments of lane slot p (components p*M + m) at step t.
 template <typename T, int D>
 __device__ __forceinline__ void draw_slot(uint64_t seed, uint64_t traj, int t, int p,
                                           int sample_type, T (&out)[comps_per_lane(D)]) {
   constexpr int P = lanes_for_dim(D), M = comps_per_lane(D);
+  if constexpr (2 * M <= 4) {
+    if (dw_steps_per_block<T>(M, sample_type) == 2) {  // the paired layout: this step's half
+      T v[2 * M];
+      draw_slot_pair<T, D>(seed, traj, t >> 1, p, sample_type, v);
+      const bool odd = (t & 1) != 0;
+#pragma unroll
+      for (int m = 0; m < M; ++m) out[m] = odd ? v[M + m] : v[m];
+      return;
+    }
+  }
   if (sample_type == DPAC_SAMPLE_BOUNDED) {
     constexpr int PB = 4, BPL = (M + PB - 1) / PB;
     const uint64_t base = ((uint64_t)t * P + p) * BPL;

@@ -391,8 +391,32 @@ __global__ __launch_bounds__(64) void k_rollout(const E eq, const DevConsts<T> c
   T disc = 1, y = 0;
   const uint64_t gtraj = (uint64_t)(a.traj_offset + lc.b);
 
+  // in-kernel Philox, paired layout (dpac_device.h): the even step of a pair draws both steps'
+  // increments; the odd step takes the half kept here (loads come in step order: pipelined())
+  constexpr bool kPairable = PHILOX && E::kP > 1 && 2 * M <= 4;
+  const bool paired = kPairable && dw_steps_per_block<T>(M, a.sample_type) == 2;
+  T pend[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) pend[m] = T(0);
   auto load = [&](int t, DwFrame<T, M>& fr) {
     if constexpr (PHILOX) {
+      if constexpr (kPairable) {
+        if (paired) {
+          if ((t & 1) == 0) {
+            T v[2 * M];
+            draw_slot_pair<T, D>(a.seed, gtraj, t >> 1, lc.p, a.sample_type, v);
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              fr.dw[m] = v[m];
+              pend[m] = v[M + m];
+            }
+          } else {
+#pragma unroll
+            for (int m = 0; m < M; ++m) fr.dw[m] = pend[m];
+          }
+          return;
+        }
+      }
       draw_owned<T, E, D>(a.seed, gtraj, t, lc.p, a.sample_type, fr.dw);
     } else if constexpr (DPAC_ABLATE == 2 || DPAC_ABLATE == 5) {
 #pragma unroll
@@ -518,23 +542,40 @@ __device__ __forceinline__ void lds_store_relaxed(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <typename T, class E, int D, int SCHEME, int OUT, int KB>
-__global__ __launch_bounds__(64 * (kStCW + 1)) void k_rollout_staged(const E eq, const DevConsts<T> c,
-                                                                      const RolloutArgs<T> a) {
+// GEN > 0 (round 6): the in-kernel Philox rollout on the same ring.  GEN
+// generator wavefronts (one per SIMD) take the loader's place and draw the workgroup's increments
+// into the ring, one counter block per lane and pass (the paired stream layout of dpac_device.h:
+// a block is one lane slot's two components at two steps), so all 64 lanes of a generator do
+// useful Philox and Box-Muller work, beside the compute wavefronts' latency-bound time loop,
+// instead of each compute lane drawing its own (6 of 16 lanes idle at d = 20).  Values and
+// arithmetic are k_rollout's Philox path's: bitwise its results.
+template <int GEN>
+constexpr int st_waves() { return kStCW + (GEN > 0 ? GEN : 1); }
+#ifndef DPAC_ST_GEN
+#define DPAC_ST_GEN 4  // generator wavefronts of the Philox variant (one per SIMD)
+#endif
+constexpr int kStGen = DPAC_ST_GEN;
+
+template <typename T, class E, int D, int SCHEME, int OUT, int KB, int GEN = 0>
+__global__ __launch_bounds__(64 * st_waves<GEN>()) void k_rollout_staged(const E eq, const DevConsts<T> c,
+                                                                          const RolloutArgs<T> a) {
   constexpr int P = E::kP, M = E::M, MC = E::MC;
   using PL = StagedPlan<T, D, P>;
   constexpr int TPW = PL::TPW, RS = PL::RS, PIECES = PL::PIECES, SLOT_LDS = PL::SLOT_LDS;
   constexpr bool COST = (OUT & kOutCost) != 0, WANT_U = (OUT & kOutU) != 0;
   constexpr int F = P < kStCH ? P : kStCH;
+  constexpr int NREADY = GEN > 0 ? GEN : 1;  // producers: the loader, or the generators
   static_assert(kStCH % F == 0 && (F & (F - 1)) == 0, "flush phase fixed per unrolled body");
+  static_assert(GEN == 0 || (2 * M <= 4 && kStCH % 2 == 0), "generators draw the paired layout");
   using TR = Transition<T, E, SCHEME>;
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[RS * SLOT_LDS];
-  __shared__ int s_ready, s_done[kStCW];
+  __shared__ int s_ready[NREADY], s_done[kStCW];
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / 64), lane = (int)threadIdx.x % 64;
   const int64_t row0 = xcd_block(blockIdx.x, gridDim.x) * TPW;
   const int N = a.N;
   if (threadIdx.x == 0) {
-    s_ready = 0;
+#pragma unroll
+    for (int w = 0; w < NREADY; ++w) s_ready[w] = 0;
 #pragma unroll
     for (int w = 0; w < kStCW; ++w) s_done[w] = 0;
   }
@@ -542,7 +583,54 @@ __global__ __launch_bounds__(64 * (kStCW + 1)) void k_rollout_staged(const E eq,
     reinterpret_cast<uint32_t*>(s_ring + (threadIdx.x / 4) * SLOT_LDS + PL::PADOFF)[threadIdx.x % 4] = 0u;
   __syncthreads();
 
-  if (wave == kStCW) {  // ---- loader: dw rows of steps t -> ring slot t % RS ----
+  if constexpr (GEN > 0) {
+    if (wave >= kStCW) {  // ---- generator g: its share of each chunk's counter blocks -> the ring ----
+      const int g = wave - kStCW;
+      const int64_t rows_live = (a.B - row0) < TPW ? (a.B - row0) : TPW;
+      constexpr int PLS = (D + M - 1) / M;                // lane slots that own components
+      constexpr int NBLK = (kStCH / 2) * TPW * PLS;       // blocks per chunk (d = 20: 8 x 16 x 10)
+      constexpr int PASSES = (NBLK + 64 * GEN - 1) / (64 * GEN);
+      constexpr int SLOT_T = SLOT_LDS / (int)sizeof(T);
+      T* const ringw = reinterpret_cast<T*>(s_ring);
+      for (int c0 = 0; c0 < N; c0 += kStCH) {
+        const int need = c0 + kStCH - RS;  // the chunk's slots were last read at steps < need
+        if (need > 0) {
+          for (;;) {
+            int mn = lds_load_relaxed(&s_done[0]);
+#pragma unroll
+            for (int w = 1; w < kStCW; ++w) mn = min(mn, lds_load_relaxed(&s_done[w]));
+            if (mn >= need) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll 1
+        for (int k = 0; k < PASSES; ++k) {
+          const int e = (k * GEN + g) * 64 + lane;
+          const int u = e / (TPW * PLS), rem = e - u * (TPW * PLS);
+          const int i = rem / PLS, p = rem - i * PLS;
+          const int t0 = c0 + 2 * u;
+          if (e < NBLK && t0 < N && i < rows_live) {
+            T v[4];
+            dw_block_values<T>(a.seed, (uint64_t)(a.traj_offset + row0 + i), (uint64_t)(t0 >> 1) * P + p,
+                               a.sample_type, v);
+            T* d0 = ringw + (t0 % RS) * SLOT_T + i * D + p * M;
+            T* d1 = ringw + ((t0 + 1) % RS) * SLOT_T + i * D + p * M;
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              if (p * M + m < D) {
+                d0[m] = v[m];
+                if (t0 + 1 < N) d1[m] = v[M + m];
+              }
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) lds_store_relaxed(&s_ready[g], c0 + kStCH < N ? c0 + kStCH : N);
+      }
+      return;
+    }
+  } else if (wave == kStCW) {  // ---- loader: dw rows of steps t -> ring slot t % RS ----
     const int64_t rows_live = (a.B - row0) < TPW ? (a.B - row0) : TPW;
     const uint32_t bytes = (uint32_t)(rows_live * D * (int64_t)sizeof(T));
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)s_ring;
@@ -583,11 +671,11 @@ __global__ __launch_bounds__(64 * (kStCW + 1)) void k_rollout_staged(const E eq,
       // the previous chunk has landed once only this chunk's copies are outstanding
       if (c0 > 0) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStCH * PIECES) : "memory");
-        if (lane == 0) lds_store_relaxed(&s_ready, c0);
+        if (lane == 0) lds_store_relaxed(&s_ready[0], c0);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) lds_store_relaxed(&s_ready, N);
+    if (lane == 0) lds_store_relaxed(&s_ready[0], N);
     return;
   }
 
@@ -664,7 +752,13 @@ __global__ __launch_bounds__(64 * (kStCW + 1)) void k_rollout_staged(const E eq,
   };
   for (int c0 = 0; c0 < N; c0 += kStCH) {
     const int want = c0 + kStCH < N ? c0 + kStCH : N;
-    while (lds_load_relaxed(&s_ready) < want) __builtin_amdgcn_s_sleep(1);
+    for (;;) {  // every producer has published the chunk
+      int mn = lds_load_relaxed(&s_ready[0]);
+#pragma unroll
+      for (int w = 1; w < NREADY; ++w) mn = min(mn, lds_load_relaxed(&s_ready[w]));
+      if (mn >= want) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
     asm volatile("" ::: "memory");
     if (c0 + kStCH <= N) {
       // RS is a multiple of kStCH: the chunk's slots are contiguous from cb
@@ -1158,6 +1252,26 @@ int run_op(const OpArgs& a) {
       constexpr int KB = rollout_kb(ring_kb((int)sizeof(DwFrame<T, E::M>), DPAC_RING_VGPRS, DPAC_ROLLOUT_KB_CAP), E::kP);
       const int out = (cost ? kOutCost : 0) | (a.u_out ? kOutU : 0);
       using SP = StagedPlan<T, D, E::kP>;
+      // the Philox variant on the ring (generator wavefronts): float, the paired stream layout
+      constexpr bool kGenOk = SP::kOk && std::is_same<T, float>::value && 2 * E::M <= 4;
+      if constexpr (kGenOk) {
+        if (philox && rollout_staged() && dw_steps_per_block<T>(E::M, a.sample_type) == 2) {
+          const dim3 sgrid((unsigned)((a.B + SP::TPW - 1) / SP::TPW)), sblock(64 * st_waves<kStGen>());
+#define DPAC_ROLL_GEN(SCH, OUT) \
+  hipLaunchKernelGGL((k_rollout_staged<T, E, D, SCH, OUT, KB, kStGen>), sgrid, sblock, 0, s, eq, c, r)
+#define DPAC_ROLL_GEN_SCH(SCH)                                 \
+  switch (out) {                                               \
+    case 0: DPAC_ROLL_GEN(SCH, 0); break;                      \
+    case kOutCost: DPAC_ROLL_GEN(SCH, kOutCost); break;        \
+    case kOutU: DPAC_ROLL_GEN(SCH, kOutU); break;              \
+    default: DPAC_ROLL_GEN(SCH, kOutCost | kOutU); break;      \
+  }
+          if (adaptive) { DPAC_ROLL_GEN_SCH(DPAC_SCHEME_ADAPTIVE) } else { DPAC_ROLL_GEN_SCH(DPAC_SCHEME_NAIVE) }
+#undef DPAC_ROLL_GEN_SCH
+#undef DPAC_ROLL_GEN
+          break;
+        }
+      }
       if constexpr (SP::kOk) {
         if (!philox && rollout_staged()) {  // dw through the loader wave's LDS ring
           const dim3 sgrid((unsigned)((a.B + SP::TPW - 1) / SP::TPW)), sblock(64 * (kStCW + 1));

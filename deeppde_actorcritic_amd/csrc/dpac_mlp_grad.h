@@ -58,15 +58,6 @@ struct PgArgs {
                           // word is set, every layer in one launch (blockIdx.z); null = always run
 };
 
-template <typename T>
-__device__ __forceinline__ T buf_load_elem(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
-  uint32_t w[sizeof(T) / 4];
-  buf_load_dwords<sizeof(T) / 4>(r, voff, w);
-  T v;
-  __builtin_memcpy(&v, &w[0], sizeof(T));
-  return v;
-}
-
 // One sub-chunk's global loads, issued before the MFMA phase of the previous one.
 template <typename T, int SR, int QB>
 struct PgStage {

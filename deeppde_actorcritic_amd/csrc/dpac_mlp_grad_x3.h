@@ -53,6 +53,9 @@ constexpr int kPgxDepth = DPAC_PGX_DEPTH;
 #endif
 static_assert(kPgxDepth == 1 || kPgxDepth == 2, "1 or 2 stages");
 constexpr float kPgxLo = 4096.f, kPgxLoInv = 1.f / 4096.f;
+#ifndef DPAC_PGW_EARLY
+#define DPAC_PGW_EARLY 1  // issue the next sub-chunk's loads before the column scaling (round 6)
+#endif
 
 // staged values of one sub-chunk (registers; loaded before the previous sub-chunk's MFMAs)
 template <int QA, int QB, bool L0>
@@ -258,6 +261,9 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
       }
       s_cmax[rb * CW + c] = m;
     }
+    // round 6: the register stage is consumed (A into the image, B into vb and the sums), so the
+    // sub-chunk kPgxDepth ahead is issued now, under the column scaling as well as the MFMAs
+    if (DPAC_PGW_EARLY && r0 + kPgxDepth * kPgxSR < r_end) issue(r0 + kPgxDepth * kPgxSR, st);
     __syncthreads();  // the column maxima of the sub-chunk
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
@@ -288,7 +294,7 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
       cexp[q] = e;
     }
     __syncthreads();
-    if (r0 + kPgxDepth * kPgxSR < r_end) issue(r0 + kPgxDepth * kPgxSR, st);  // lands kPgxDepth sub-chunks later
+    if (!DPAC_PGW_EARLY && r0 + kPgxDepth * kPgxSR < r_end) issue(r0 + kPgxDepth * kPgxSR, st);  // lands kPgxDepth sub-chunks later
     pgh8 bh[NTJ], bl[NTJ], b12[NTJ];
 #pragma unroll
     for (int jj = 0; jj < NTJ; ++jj) {
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
 
   // the 32 rows at r0: z_l and z_{l+1} rows by LDS-DMA (wavefront w: rows 2w, 2w + 1),
   // G_{l+1} through registers with one descriptor per row (wave-uniform rb)
-  auto issue = [&](int64_t r0) {
+  auto issue_dma = [&](int64_t r0) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int i = 2 * wave + j;
@@ -542,12 +548,18 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
       if constexpr (L0) pgw_row_dma(a.G + a.goff[0] + row * a.gtot, voffA, smem + PL::kRawG0 + i * CW * 4);
       else if (rt0) pgw_row_dma_128(a.G + a.goff[0] + row * a.gtot, (uint32_t)K * 4u, lane, smem + PL::kSmem + i * 128);
     }
+  };
+  auto issue_g = [&](int64_t r0) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int64_t row = r0 + 8 * rbu + i;
       const auto rB = make_rsrc(gB + row * a.gtot, row < r_end ? (uint32_t)H * 4u : 0u);
       gst[i] = buf_load_elem<float>(rB, offB);
     }
+  };
+  auto issue = [&](int64_t r0) {
+    issue_dma(r0);
+    issue_g(r0);
   };
 
   const int fq = lane >> 4, fi = lane & 15;
@@ -597,6 +609,11 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
       s_cmax[rb * CW + fl] = m;
     }
     __syncthreads();  // the column maxima; every raw row read
+    // round 6: the next sub-chunk's raw rows (LDS-DMA: no registers) are issued here, as soon as
+    // every raw row is read, so they land during the column scaling and split as well as the
+    // MFMAs; its G rows (a register stage) after the split as before (DPAC_PGW_EARLY=0: all after
+    // the split, rounds 4-5)
+    if (DPAC_PGW_EARLY && r0 + kPgxSR < r_end) issue_dma(r0 + kPgxSR);
     {
       const float m = fmaxf(fmaxf(s_cmax[fl], s_cmax[CW + fl]), fmaxf(s_cmax[2 * CW + fl], s_cmax[3 * CW + fl]));
       int e = cexp;
@@ -624,7 +641,10 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
     }
     // the next sub-chunk's rows (the raw rows are read; vb no longer needs gst): they land
     // during this sub-chunk's MFMAs
-    if (r0 + kPgxSR < r_end) issue(r0 + kPgxSR);
+    if (r0 + kPgxSR < r_end) {
+      if (DPAC_PGW_EARLY) issue_g(r0 + kPgxSR);  // the G register stage: live only from here
+      else issue(r0 + kPgxSR);
+    }
     __syncthreads();  // the images
     {
       const pgh8 bh = *reinterpret_cast<const pgh8*>(bBase);

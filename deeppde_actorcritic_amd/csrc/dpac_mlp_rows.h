@@ -84,13 +84,36 @@ struct MrArgs {
   const uint32_t* guard;
 };
 
-// (sigma(x,u) dw)_j of row r (0 past d).
+// The TD1 operands (x, u, dw) of one row block [row0, row0 + live) through buffer descriptors
+// sized to exactly those rows (round 6): a row past the block reads 0, never memory past the
+// arrays (round 5's fault: a dead 16-row block read its first row's sigma dw through plain
+// pointers, up to 48 rows past the end of dw).
 template <typename T>
-__device__ __forceinline__ T td_sdw(const MrArgs<T>& a, int64_t r, int j, int d) {
-  if (j >= d) return T(0);
-  T s = a.td_sa;
-  if (a.td_sb != T(0)) s = a.td_sa * (1 + (a.td_sb * a.td_x[r * a.td_ldx + j]) * a.td_u[r * a.td_ldu + j]);
-  return s * a.td_dw[r * d + j];
+struct TdSrc {
+  __amdgpu_buffer_rsrc_t x, u, dw;
+  int64_t row0;
+  int live, ldx, ldu, d;
+  T sa, sb;
+};
+
+template <typename T>
+__device__ __forceinline__ TdSrc<T> td_src(const MrArgs<T>& a, int64_t row0, int live, int d) {
+  return TdSrc<T>{rows_rsrc(a.td_x, row0, live, a.td_ldx), rows_rsrc(a.td_u, row0, live, a.td_ldu),
+                  rows_rsrc(a.td_dw, row0, live, d), row0, live, (int)a.td_ldx, (int)a.td_ldu, d, a.td_sa,
+                  a.td_sb};
+}
+
+// (sigma(x,u) dw)_j of row r (0 past d, and 0 for a row outside the block).
+template <typename T>
+__device__ __forceinline__ T td_sdw(const TdSrc<T>& t, int64_t r, int j) {
+  if (j >= t.d) return T(0);
+  DPAC_CHECK_ROW(r - t.row0, t.live);
+  const uint32_t o = (uint32_t)(r - t.row0);
+  T s = t.sa;
+  if (t.sb != T(0))
+    s = t.sa * (1 + (t.sb * buf_load_elem<T>(t.x, (o * (uint32_t)t.ldx + (uint32_t)j) * (uint32_t)sizeof(T))) *
+                        buf_load_elem<T>(t.u, (o * (uint32_t)t.ldu + (uint32_t)j) * (uint32_t)sizeof(T)));
+  return s * buf_load_elem<T>(t.dw, (o * (uint32_t)t.d + (uint32_t)j) * (uint32_t)sizeof(T));
 }
 
 template <int P, typename T>
@@ -110,9 +133,11 @@ __device__ __forceinline__ bool td_prefetch(const MrArgs<T>& a, int64_t row0, in
   const int P = a.td_p, M = (d + P - 1) / P;
   if (!a.gdot || ROWS != kMrThreads / 16 || M > kTdPre) return false;
   const int l16 = tid % 16, rr = tid / 16;
-  const int64_t r = row0 + (rr < rows_live ? rr : 0);
+  const TdSrc<T> src = td_src(a, row0, rows_live, d);
+  const int64_t r = row0 + rr;  // past the block: reads 0 (unused: td_dot_rows stores live rows only)
 #pragma unroll
-  for (int m = 0; m < kTdPre; ++m) pre[m] = (l16 < P && m < M) ? td_sdw(a, r, l16 * M + m, d) : T(0);
+  for (int m = 0; m < kTdPre; ++m)
+    pre[m] = (l16 < P && m < M && rr < rows_live) ? td_sdw(src, r, l16 * M + m) : T(0);
   return true;
 }
 
@@ -125,6 +150,7 @@ __device__ __forceinline__ void td_dot_rows(const MrArgs<T>& a, const T* G, int6
                                             int d, int tid, bool have_pre, const T (&pre)[kTdPre]) {
   if (rows_live <= 0) return;  // uniform over the call's threads
   const int l16 = tid % 16, P = a.td_p, M = (d + P - 1) / P;
+  const TdSrc<T> src = td_src(a, row0, rows_live, d);
   for (int rr = tid / 16; rr < ROWS; rr += kMrThreads / 16) {
     const int64_t r = row0 + (rr < rows_live ? rr : 0);
     T acc = T(0);
@@ -140,7 +166,7 @@ __device__ __forceinline__ void td_dot_rows(const MrArgs<T>& a, const T* G, int6
         for (int m = 0; m < M; ++m) {
           const int j = l16 * M + m;
           const T g = j < d ? G[rr * kMrLd + j] : T(0);
-          const T sdw = td_sdw(a, r, j, d);
+          const T sdw = td_sdw(src, r, j);
           acc = m == 0 ? sdw * g : fma(sdw, g, acc);
         }
       }
@@ -433,10 +459,14 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_fwd(const MrArgs<T> a) 
     const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
     const int d = a.width[0];
     // a_0 = BN_0(x) into image 0 (solver.py:265); everything else zero
+    const __amdgpu_buffer_rsrc_t rx = rows_rsrc(a.x, row0, rows_live, a.ldx);
     for (int e = tid; e < ROWS * kMrLd; e += kMrThreads) {
       const int r = e / kMrLd, k = e % kMrLd;
       T v = T(0);
-      if (k < d && r < rows_live) v = a.shift[0][k] + a.x[(row0 + r) * a.ldx + k] * a.scale[0][k];
+      if (k < d && r < rows_live) {
+        DPAC_CHECK_ROW(r, rows_live);
+        v = a.shift[0][k] + buf_load_elem<T>(rx, (uint32_t)(r * a.ldx + k) * (uint32_t)sizeof(T)) * a.scale[0][k];
+      }
       s_img[0][e] = v;
       s_img[1][e] = T(0);
     }
@@ -472,12 +502,16 @@ __global__ __launch_bounds__(kMrThreads) void k_mlp_rows_bwd(const MrArgs<T> a) 
     const int64_t row0 = blk * ROWS;
     const int rows_live = (int)((a.rows - row0) < ROWS ? (a.rows - row0) : ROWS);
     // G_{L+1} = dL/d out: into image 0 and to G
+    const TdSrc<T> src = td_src(a, row0, rows_live, hout);
+    const __amdgpu_buffer_rsrc_t rgd = rows_rsrc(a.g_gdot, row0, rows_live, 1);
+    const __amdgpu_buffer_rsrc_t rgo = rows_rsrc(a.g_out, row0, rows_live, hout);
     for (int e = tid; e < ROWS * kMrLd; e += kMrThreads) {
       const int r = e / kMrLd, k = e % kMrLd;
       T v = T(0);
       if (k < hout && r < rows_live) {
-        v = a.g_gdot ? a.g_gdot[row0 + r] * td_sdw(a, row0 + r, k, hout)  // td_assemble_bwd's product
-                     : a.g_out[(row0 + r) * hout + k];
+        DPAC_CHECK_ROW(r, rows_live);
+        v = a.g_gdot ? buf_load_elem<T>(rgd, (uint32_t)r * (uint32_t)sizeof(T)) * td_sdw(src, row0 + r, k)
+                     : buf_load_elem<T>(rgo, (uint32_t)(r * hout + k) * (uint32_t)sizeof(T));  // td_assemble_bwd's product
         a.G[(row0 + r) * a.gtot + a.goff[L + 1] + k] = v;
       }
       s_img[0][e] = v;

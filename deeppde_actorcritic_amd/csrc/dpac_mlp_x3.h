@@ -487,6 +487,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t x3_rows_rsrc(const float* base
   return make_rsrc(base ? base + row0 * ld : nullptr, base ? (uint32_t)(live * ld * 4) : 0u);
 }
 
+// x[row0 + r][k] of the forward's row block through its row descriptor (0 past the block)
+__device__ __forceinline__ float x3_x_at(__amdgpu_buffer_rsrc_t rx, int r, int k, int64_t ldx, int live) {
+  DPAC_CHECK_ROW(r, live);
+  return buf_load_elem<float>(rx, (uint32_t)(r * ldx + k) * 4u);
+}
+
 __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char x3_lds[];
   _Float16* const img0 = reinterpret_cast<_Float16*>(x3_lds);
@@ -498,6 +504,7 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
   const int64_t row0 = (int64_t)blockIdx.x * kX3Rows;
   const int rows_live = (int)((a.rows - row0) < kX3Rows ? (a.rows - row0) : kX3Rows);
   const int d = a.width[0];
+  const __amdgpu_buffer_rsrc_t rx0 = rows_rsrc(a.x, row0, rows_live, a.ldx);
   bool bad = false;  // an operand outside the split range (dpac.h dpac_mlp.status)
   X3_MARK(0);
   // a_0 = BN_0(x) (solver.py:265): for d <= 32 the loads go first, their latency under the
@@ -508,7 +515,7 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
 #pragma unroll
   for (int t = 0; t < kPro; ++t) {
     const int e = tid + t * kX3Threads, r = e / d, k = e % d;
-    xv[t] = (narrow && e < kX3Rows * d && r < rows_live) ? a.x[(row0 + r) * a.ldx + k] : 0.f;
+    xv[t] = (narrow && e < kX3Rows * d && r < rows_live) ? x3_x_at(rx0, r, k, a.ldx, rows_live) : 0.f;
   }
   x3_zero(img0, tid);
   x3_zero(img1, tid);
@@ -522,7 +529,7 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
   } else {
     for (int e = tid; e < kX3Rows * d; e += kX3Threads) {
       const int r = e / d, k = e % d;
-      bad |= x3_put(img0, r, k, r < rows_live ? a.shift[0][k] + a.x[(row0 + r) * a.ldx + k] * a.scale[0][k] : 0.f);
+      bad |= x3_put(img0, r, k, r < rows_live ? a.shift[0][k] + x3_x_at(rx0, r, k, a.ldx, rows_live) * a.scale[0][k] : 0.f);
     }
   }
   MrArgs<float> ta{};  // the TD1 operands, as dpac_mlp_rows.h's td_dot_rows reads them
@@ -596,9 +603,18 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
     const int r = tid / 8, sub = tid % 8;  // 8 lanes per row (kX3RowsB rows: the first 8 kX3RowsB threads)
     const bool live = r < rows_live;
     const int64_t gr = row0 + (live ? r : 0);
+    const TdSrc<float> src = td_src(ta, row0, rows_live, hout);
+    const __amdgpu_buffer_rsrc_t rgd = rows_rsrc(a.g_gdot, row0, rows_live, 1);
+    const __amdgpu_buffer_rsrc_t rgo = rows_rsrc(a.g_out, row0, rows_live, hout);
+    auto g_top = [&](int k) {  // dL/d out of row gr, column k (0 for a dead row)
+      DPAC_CHECK_ROW(gr - row0, rows_live);
+      const uint32_t o = (uint32_t)(gr - row0);
+      return a.g_gdot ? buf_load_elem<float>(rgd, o * 4u) * td_sdw(src, gr, k)
+                      : buf_load_elem<float>(rgo, (o * (uint32_t)hout + (uint32_t)k) * 4u);
+    };
     float mx = 0.f;
     for (int k = sub; k < hout; k += 8) {
-      const float v = live ? (a.g_gdot ? a.g_gdot[gr] * td_sdw(ta, gr, k, hout) : a.g_out[gr * hout + k]) : 0.f;
+      const float v = live ? g_top(k) : 0.f;
       if (live) a.G[gr * a.gtot + a.goff[L + 1] + k] = v;
       mx = fmaxf(mx, fabsf(v));
     }
@@ -608,7 +624,7 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
     if (mx > 0.f && mx < 3.0e38f) (void)frexpf(mx, &e);  // mx in [2^(e-1), 2^e)
     const float sc = ldexpf(1.f, 1 - e);                   // max |G| * sc in [1, 2)
     for (int k = sub; k < hout; k += 8) {
-      const float v = live ? (a.g_gdot ? a.g_gdot[gr] * td_sdw(ta, gr, k, hout) : a.g_out[gr * hout + k]) : 0.f;
+      const float v = live ? g_top(k) : 0.f;
       if (r < kX3RowsB) bad |= x3_put(img0, r, k, v * sc);
     }
     if (sub == 0 && r < kX3RowsB) rinv[r] = ldexpf(1.f, e - 1);

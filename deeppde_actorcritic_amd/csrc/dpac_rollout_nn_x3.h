@@ -97,14 +97,47 @@ __device__ __forceinline__ bool nx_split4(nxf4 v, nxh4& h, nxh4& l) {
   return x3_bad4(v[0], v[1], v[2], v[3]);
 }
 
-// four consecutive features f0..f0+3 (f0 % 4 == 0) of one row, split, as two 8-byte LDS writes;
-// true if one of them is outside the split range (dpac.h dpac_mlp.status)
-__device__ __forceinline__ bool nx_put4(_Float16* img, int ld, int row, int f0, nxf4 v) {
+// Bank-conflict-free hidden images (round 6).  A row holds, per 32-k chunk,
+// 32 hi halves then 32 lo halves: eight 16-byte blocks.  The B-operand reads (lane l: row l & 15,
+// k block l >> 4, ds_read_b128) were conflict-free at the 264-dword row stride, but the
+// epilogue's two 8-byte writes per tile (ds_write_b64: 16 contiguous lanes = the 16 rows at one
+// k quad, banks (a/4) mod 32, row stride 8 mod 32) hit 4 distinct bank pairs: 4-way conflicts,
+// the bulk of the kernels' measured lds_conflict_frac (0.32 / 0.36).  Now:
+//  * the 16-byte blocks of rows 4..7 and 12..15 swap in pairs (block index XOR ((row >> 2) & 1));
+//  * a v_permlane16_swap per dword gives the lanes of even 16-lane rows (k quads 0, 2) the hi
+//    halves of their quad AND the next quad, and the odd rows the lo halves of both, so each
+//    lane stores ONE 16-byte block (ds_write_b128, 8 contiguous lanes per bank cycle).
+// Both the reads and the writes are then conflict-free under gfx950's LDS lane grouping
+// (MI355X_MICROARCH.md §LDS; checked exhaustively for every tile and chunk offline).
+#ifndef DPAC_NX_SWZ
+#define DPAC_NX_SWZ 0  // 0: unswizzled images, two 8-byte writes per tile (4-way write conflicts);
+                       // 1: swizzled, two 8-byte writes (2-way); 2: swizzled + permlane16 swap, one
+                       // 16-byte write (conflict-free)
+#endif
+__device__ __forceinline__ int nx_swz(int row) { return DPAC_NX_SWZ ? (row >> 2) & 1 : 0; }
+
+// four consecutive features f0..f0+3 (f0 % 4 == 0) of one row, split; the wave's lanes exchange
+// halves (above) and each stores one 16-byte block.  ld = kNxLd (the swizzled hidden images).
+// True if one of the values is outside the split range (dpac.h dpac_mlp.status).
+__device__ __forceinline__ bool nx_put4(_Float16* img, int ld, int row, int f0, nxf4 v, int lane) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   nxh4 h, l;
   const bool bad = nx_split4(v, h, l);
-  _Float16* p = img + row * ld + (f0 >> 5) * 64 + (f0 & 31);
-  *reinterpret_cast<nxh4*>(p) = h;
-  *reinterpret_cast<nxh4*>(p + 32) = l;
+  if constexpr (DPAC_NX_SWZ < 2) {  // two 8-byte writes: hi at block (f0 % 32) / 8, lo 4 blocks on
+    const int blk = ((f0 & 31) >> 3) ^ nx_swz(row);  // (a 4-feature quad is half a block)
+    _Float16* p = img + row * ld + (f0 >> 5) * 64 + 8 * blk + (f0 & 4);
+    *reinterpret_cast<nxh4*>(p) = h;
+    *reinterpret_cast<nxh4*>(p + 32) = l;
+    return bad;
+  }
+  u32x2 hw = __builtin_bit_cast(u32x2, h), lw = __builtin_bit_cast(u32x2, l);
+  // odd 16-lane rows of hw <-> even rows of lw: even rows keep [h(q) | h(q + 1)], odd rows
+  // [l(q - 1) | l(q)]
+  const auto s0 = __builtin_amdgcn_permlane16_swap(hw[0], lw[0], false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(hw[1], lw[1], false, false);
+  const int q = lane >> 4;
+  _Float16* p = img + row * ld + (f0 >> 5) * 64 + 32 * (q & 1) + 16 * ((f0 >> 4) & 1) + 8 * ((q >> 1) ^ nx_swz(row));
+  *reinterpret_cast<uint4*>(p) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
   return bad;
 }
 
@@ -208,7 +241,9 @@ __device__ __forceinline__ void nx_prod(const _Float16* in, int c0, nxh8 (&wh)[N
                                         nxf4 (&acc)[2][3], int lane, const _Float16* W = nullptr, int Nout = 0,
                                         int nch = 0, int tA = 0, int tB = 0) {
   static_assert(RING ? NS == RING : NS == NC, "resident: one slot per chunk");
-  const _Float16* b = in + (lane & 15) * LD + c0 * 64 + 8 * (lane >> 4);
+  // the hidden images' 16-byte blocks are swizzled by row (nx_swz); the narrow input image is not
+  const int kq = LD == kNxLd ? ((lane >> 4) ^ nx_swz(lane & 15)) : (lane >> 4);
+  const _Float16* b = in + (lane & 15) * LD + c0 * 64 + 8 * kq;
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -328,7 +363,7 @@ __device__ __forceinline__ bool nx_fwd_epi(const nxf4 (&acc)[2][3], int wave, in
         bl[4 * j + e] = l[e];
       }
     } else {
-      bad |= nx_put4(out, kNxLd, row, f0, y);
+      bad |= nx_put4(out, kNxLd, row, f0, y, lane);
     }
     if constexpr (MASK && !(DPAC_NX_ABLATE & 2)) {
       const uint32_t w = nx_quad_gather(nib, lane);
@@ -382,7 +417,7 @@ __device__ __forceinline__ bool nx_bwd_epi(const nxf4 (&acc)[2][3], int wave, in
         bl[4 * j + e] = l[e];
       }
     } else {
-      bad |= nx_put4(out, kNxLd, row, f0, v);
+      bad |= nx_put4(out, kNxLd, row, f0, v, lane);
     }
   }
   if constexpr (FOLD) nx_fold_prod(*fh, *fl, bh, bl, part, wave, lane);

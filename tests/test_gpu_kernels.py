@@ -203,14 +203,17 @@ def test_sampler_distribution_and_sharding(dtype):
     assert torch.all(x00 == torch.tensor(0.01, dtype=dtype))
 
 
+@pytest.mark.parametrize("N", [64, 63])
 @pytest.mark.parametrize("name,d", [("LQR", 20), ("LQR", 5), ("VDP", 20), ("EKN", 10)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("sample_type", [_lib.SAMPLE_NORMAL, _lib.SAMPLE_BOUNDED])
-def test_inkernel_philox_equals_sampled_dw(name, d, dtype, sample_type):
-    """dw=None draws the same numbers in-kernel as dpac_sample writes to HBM."""
-    cfg = eqn_config(name, d, N=64)
+def test_inkernel_philox_equals_sampled_dw(name, d, dtype, sample_type, N):
+    """dw=None draws the same numbers in-kernel as dpac_sample writes to HBM (round 6: the paired
+    layout, one counter block per lane slot and step pair, with an odd horizon's unpaired last
+    step; the TD kernel's horizon chunks start at odd steps too)."""
+    cfg = eqn_config(name, d, N=N)
     eqp = pe(cfg).params()
-    B, N = 1000, 64
+    B = 1000
     x0, dw, _ = ops.sample(eqp, sample_type, B, N, seed=9, traj_offset=123, dtype=dtype, device=DEV)
     a = ops.rollout_analytic(eqp, 1, x0, dw, 0.2, N, cost_order=_lib.COST_ACTOR)
     b = ops.rollout_analytic(eqp, 1, x0, None, 0.2, N, seed=9, traj_offset=123, sample_type=sample_type,
@@ -306,3 +309,56 @@ def test_staged_rollout_bitwise(name, d, B, N, scheme, dtype):
             assert (s is None) == (t is None)
             if s is not None:
                 assert torch.equal(s, t)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("sample_type", [_lib.SAMPLE_NORMAL, _lib.SAMPLE_BOUNDED])
+def test_sampler_stream_is_a_function_of_step_and_component(dtype, sample_type):
+    """The dw stream depends only on (seed, global trajectory, step, component): a shorter
+    horizon (odd or even) draws the leading steps of a longer one bit for bit, and a shard keeps
+    its rows (the paired layout keeps both properties)."""
+    eqp = pe(eqn_config("LQR", 20)).params()
+    B = 777
+    _, dw, _ = ops.sample(eqp, sample_type, B, 50, seed=5, dtype=dtype, device=DEV)
+    for n in (1, 2, 7, 49):
+        _, dws, _ = ops.sample(eqp, sample_type, B, n, seed=5, dtype=dtype, device=DEV)
+        assert torch.equal(dws, dw[:n])
+    _, dwo, _ = ops.sample(eqp, sample_type, 100, 49, seed=5, traj_offset=300, dtype=dtype, device=DEV)
+    assert torch.equal(dwo, dw[:49, 300:400])
+    # consecutive steps are independent draws, not copies (the two halves of a block)
+    c = float(torch.corrcoef(torch.stack([dw[0::2].double().reshape(-1)[:100000],
+                                          dw[1::2].double().reshape(-1)[:100000]]))[0, 1])
+    assert abs(c) < 0.02, c
+
+
+@pytest.mark.parametrize("sample_type", [_lib.SAMPLE_NORMAL, _lib.SAMPLE_BOUNDED])
+@pytest.mark.parametrize("scheme", ["adaptive", "naive"])
+@pytest.mark.parametrize("name,d,B,N", [("LQR", 20, 4096, 200), ("LQR", 20, 300, 37), ("EKN", 20, 65, 16),
+                                        ("LQR_var", 10, 33, 101), ("LQR", 5, 37, 13), ("VDP", 20, 70, 30)])
+def test_inkernel_philox_generator_rollout_bitwise(name, d, B, N, scheme, sample_type):
+    """Round 6: the in-kernel Philox rollout with the increments drawn by
+    generator wavefronts into the staged kernel's LDS ring (k_rollout_staged<..., GEN = 4>, the
+    default for float) gives bitwise the results of k_rollout drawing them in each compute lane
+    (DPAC_ROLLOUT_STAGED=0): odd horizons (a last unpaired step), partial workgroups, chunks that
+    wrap the ring, the u and cost outputs (VDP and float64 keep k_rollout)."""
+    cfg = eqn_config(name, d, T=0.2, N=N)
+    eqp = pe(cfg).params()
+    sch = SCHEMES[scheme]
+    x0, _, _ = ops.sample(eqp, sample_type, B, N, seed=11, traj_offset=5, device=DEV)
+    out = {}
+    old = os.environ.get("DPAC_ROLLOUT_STAGED")
+    try:
+        for k in ("0", "1"):
+            os.environ["DPAC_ROLLOUT_STAGED"] = k
+            out[k] = [ops.rollout_analytic(eqp, sch, x0, None, 0.2, N, seed=11, traj_offset=5, sample_type=sample_type,
+                                           want_u=wu, cost_order=co)
+                      for wu, co in ((False, None), (True, _lib.COST_ACTOR))]
+    finally:
+        if old is None:
+            os.environ.pop("DPAC_ROLLOUT_STAGED", None)
+        else:
+            os.environ["DPAC_ROLLOUT_STAGED"] = old
+    for ra, rb in zip(out["0"], out["1"]):
+        for ta, tb in zip(ra, rb):
+            if ta is not None:
+                assert torch.equal(ta, tb)

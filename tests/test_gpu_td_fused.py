@@ -14,6 +14,7 @@ The split path itself is checked against the oracle in test_gpu_kernels.py /
 test_gpu_models.py.
 """
 import ctypes
+import os
 
 import pytest
 import torch
@@ -155,3 +156,33 @@ def test_fused_td1_dead_row_blocks_read_nothing_past_the_end(name, d):
     ref = torch.sum(sig * dw * G, 1)  # another summation order than the kernel's DPP tree
     assert torch.allclose(gdot, ref, rtol=1e-5, atol=1e-6)
     del bx, bu, bd
+
+
+_BOUNDS_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "variants",
+                           "libdpac_bounds.so")
+
+
+@pytest.mark.parametrize("math", ["x3", "f32"])
+@pytest.mark.parametrize("lib", ["main", "bounds"])
+def test_row_kernels_ragged_rows_in_a_fresh_process_without_the_caching_allocator(lib, math):
+    """VERDICT r05 item 6 / ADVICE r05: tests/bounds_check.py in a fresh process with
+    PYTORCH_NO_CUDA_MEMORY_CACHING=1 (every buffer its own hipMalloc, each operand a view ending
+    exactly at the end of its allocation), the row kernels' TD1 operands and prologue reads over
+    ragged row counts — once with the shipped library (the loads go through row descriptors
+    since round 6: a dead row reads 0) and once with the DPAC_CHECK_BOUNDS build, whose every
+    row-indexed load checks its row and prints a violation line otherwise."""
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTORCH_NO_CUDA_MEMORY_CACHING="1", DPAC_MLP_MATH=math)
+    if lib == "bounds":
+        if not os.path.exists(_BOUNDS_LIB):
+            pytest.skip("tools/variants/libdpac_bounds.so not built (make bounds)")
+        env["DPAC_LIB"] = _BOUNDS_LIB
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-u", os.path.join(root, "tests", "bounds_check.py")], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=180)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "bounds_check ok" in r.stdout, out[-3000:]
+    assert "dpac bounds violation" not in out, out[-3000:]
+    print(r.stdout.strip().splitlines()[-1])

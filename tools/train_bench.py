@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--config", default="lqr_d20", help="a BASELINE config: lqr_d20, ekn_d20, lqr_var_d20, vdp_d20")
     a = ap.parse_args()
+    torch.cuda.reset_peak_memory_stats()
     cfg = lqr_d20(a.iters, 10 ** 9, a.dtype, a.batch, a.batch, name=a.config)
     sp = psol.ActorCriticSolver(cfg, getattr(peq, cfg.eqn_config.eqn_name)(cfg.eqn_config), seed=1,
                                 sampler="device")
@@ -74,7 +75,9 @@ def main():
                       "ms_per_iter": ms, "sequential_ms": (tc + ta) / a.iters * 1e3,
                       "critic_ms": tc / a.iters * 1e3, "actor_ms": ta / a.iters * 1e3,
                       "host_submit_ms": th / a.iters * 1e3,
-                      "traj_steps_per_s": 2 * B * N / (ms * 1e-3)}), flush=True)
+                      "traj_steps_per_s": 2 * B * N / (ms * 1e-3), "graph_sets": psol.GRAPH_SETS,
+                      "peak_allocated_GB": torch.cuda.max_memory_allocated() / 1e9,
+                      "peak_reserved_GB": torch.cuda.max_memory_reserved() / 1e9}), flush=True)
 
 
 if __name__ == "__main__":
