@@ -199,7 +199,7 @@ def training_variant(name, dtype, B, world=1, iters=6, warmup=3, par=None, total
             "mlp": "20-200-200-200-%d" % cfg.eqn_config.control_dim, "ms_per_iteration": ms,
             "traj_steps_per_s": 2 * Bg * N / (ms * 1e-3),
             "mlp_executed_TFLOPs": 7 * rate, "mlp_reference_equiv_TFLOPs": 11 * rate,
-            "mlp_math": ops_mlp_math(dtype), "collectives": coll, "graph_sets": psol.GRAPH_SETS,
+            "mlp_math": ops_mlp_math(dtype), "collectives": coll, "graph_sets": psol.graph_sets(B),
             "peak_memory_GB": (torch.cuda.max_memory_allocated() - mem0) / 1e9,
             "peak_memory_note": "device memory this variant's solver, samples and HIP graph pools held at "
                                 "their peak, above what was allocated before it (torch caching allocator)"}

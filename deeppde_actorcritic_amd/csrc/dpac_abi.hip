@@ -196,37 +196,36 @@ int launch(const OpArgs& a) {
 // Sampler kernels (equation.py:13-44), stream layout in dpac_device.h.
 // ---------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int N, int D, int sample_type,
+__global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int64_t b0, int nb, int N, int D, int sample_type,
                                                    uint64_t seed, int64_t traj_offset, T* dw) {
-  // one thread per (unit u, b, lane slot p, block): the stream layout of draw_slot(); a unit is
-  // a step pair in the paired layout (S = 2), else one step
+  // thread (unit u, trajectory b0 + bl, lane slot p, block): the stream layout of draw_slot(); a
+  // unit is a step pair in the paired layout (S = 2), else one step.  x runs over this launch's
+  // (bl, p, block) in 32-bit arithmetic, y over the units (round 6: one 64-bit division chain per
+  // block cost more than its Philox rounds)
   const int P = lanes_for_dim(D), M = comps_per_lane(D);
   const int PB = dw_per_block<T>(sample_type);
   const int S = dw_steps_per_block<T>(M, sample_type);
   const int BPU = S == 2 ? 1 : (M + PB - 1) / PB;  // counter blocks per (unit, lane slot)
-  const int64_t units = S == 2 ? (N + 1) / 2 : N;
-  const int PL = (D + M - 1) / M;  // lane slots that own components (d = 20: 10 of P = 16)
-  (void)P;
-  const int64_t per_row = (int64_t)PL * BPU;  // counter blocks per (unit, b)
-  const int64_t total = units * B * per_row;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t ub = i / per_row;
-    const int rem = (int)(i - ub * per_row);
-    const int p = rem / BPU, blk = rem % BPU;
-    const int u = (int)(ub / B);
-    const int64_t b = ub - (int64_t)u * B;
-    const uint64_t traj = (uint64_t)(traj_offset + b);
+  const int units = S == 2 ? (N + 1) / 2 : N;
+  const int PL = (D + M - 1) / M;                  // lane slots that own components (d = 20: 10 of 16)
+  const uint32_t per_b = (uint32_t)(PL * BPU);
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  if (idx >= (uint32_t)nb * per_b) return;
+  const uint32_t bl = idx / per_b, rem = idx - bl * per_b;
+  const int p = (int)rem / BPU, blk = (int)rem - p * BPU;
+  const int64_t b = b0 + bl;
+  const uint64_t traj = (uint64_t)(traj_offset + b);
+  for (int u = blockIdx.y; u < units; u += gridDim.y) {
     T vals[4];
-    dw_block_values<T>(seed, traj, ((uint64_t)u * lanes_for_dim(D) + p) * BPU + blk, sample_type, vals);
+    dw_block_values<T>(seed, traj, ((uint64_t)u * P + p) * BPU + blk, sample_type, vals);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if (e >= PB) break;
-      const int idx = blk * PB + e;  // the value's place in the lane slot's unit
-      const int t = S == 2 ? 2 * u + idx / M : u;
-      const int m = S == 2 ? idx % M : idx;
+      const int iv = blk * PB + e;  // the value's place in the lane slot's unit
+      const int t = S == 2 ? 2 * u + iv / M : u;
+      const int m = S == 2 ? iv % M : iv;
       const int j = p * M + m;
-      if ((S == 2 ? idx < 2 * M : m < M) && t < N && j < D) dw[((int64_t)t * B + b) * D + j] = vals[e];
+      if ((S == 2 ? iv < 2 * M : m < M) && t < N && j < D) dw[((int64_t)t * B + b) * D + j] = vals[e];
     }
   }
 }
@@ -290,15 +289,18 @@ int sample_impl(const dpac_eqn_params* eq, int32_t sample_type, int64_t B, int32
                 uint64_t seed, int64_t off, void* x0, void* dw, void* x_bdry, hipStream_t s) {
   const int D = eq->dim;
   if (dw) {
-    const int P = lanes_for_dim(D), M = comps_per_lane(D);
+    const int M = comps_per_lane(D);
     const int st = sample_type == DPAC_SAMPLE_ZERO_X0 ? DPAC_SAMPLE_NORMAL : sample_type;
     const int PB = dw_per_block<T>(st), S = dw_steps_per_block<T>(M, st);
-    const int PL = (D + M - 1) / M;  // lane slots that own components
-    (void)P;
-    const int64_t total = (S == 2 ? ((int64_t)N + 1) / 2 : (int64_t)N) * B * PL * (S == 2 ? 1 : (M + PB - 1) / PB);
-    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 65536);
-    hipLaunchKernelGGL(k_sample_dw<T>, dim3((unsigned)blocks), dim3(256), 0, s, B, N, D, st, seed,
-                       off, (T*)dw);
+    const int per_b = ((D + M - 1) / M) * (S == 2 ? 1 : (M + PB - 1) / PB);
+    const int units = S == 2 ? (N + 1) / 2 : N;
+    const int64_t chunk = (int64_t)1 << 24;  // trajectories per launch: 32-bit thread indices
+    for (int64_t b0 = 0; b0 < B; b0 += chunk) {
+      const int nb = (int)std::min<int64_t>(chunk, B - b0);
+      const dim3 g((unsigned)(((int64_t)nb * per_b + 255) / 256), (unsigned)std::min(units, 65535));
+      hipLaunchKernelGGL(k_sample_dw<T>, g, dim3(256), 0, s, B, b0, nb, N, D, st, seed, off, (T*)dw);
+      if (hipError_t e = hipGetLastError()) return (int)e;
+    }
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
   if (x0 || x_bdry) {

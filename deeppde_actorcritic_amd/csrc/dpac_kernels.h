@@ -552,7 +552,7 @@ __device__ __forceinline__ void lds_store_relaxed(int* p, int v) {
 template <int GEN>
 constexpr int st_waves() { return kStCW + (GEN > 0 ? GEN : 1); }
 #ifndef DPAC_ST_GEN
-#define DPAC_ST_GEN 4  // generator wavefronts of the Philox variant (one per SIMD)
+#define DPAC_ST_GEN 12  // generator wavefronts of the Philox variant (three per SIMD; round 6: 2 / 4 / 8 / 12 measured)
 #endif
 constexpr int kStGen = DPAC_ST_GEN;
 

@@ -467,12 +467,27 @@ class _SplitCriticGraphs:
             self.g_redo.replay()
 
 
-# DPAC_GRAPH_SETS=2 (default): train_iteration alternates two sets of the split graphs and
-# prefetch_samples draws the next iteration's samples into the idle set's static inputs (no
-# copies in front of the graphs); 1: one set, the samples copied in (round 4's path).
-GRAPH_SETS = int(os.environ.get("DPAC_GRAPH_SETS", "2"))
-if GRAPH_SETS not in (1, 2):
-    raise ValueError(f"DPAC_GRAPH_SETS must be 1 or 2, got {GRAPH_SETS}")
+# DPAC_GRAPH_SETS=2: train_iteration alternates two sets of the split graphs and prefetch_samples
+# draws the next iteration's samples into the idle set's static inputs (no copies in front of the
+# graphs; round 5); 1: one set, the samples copied in (round 4's path).  "auto" (default, round 6):
+# two sets while a rank's batch is at most GRAPH_SETS_MAX_ROWS trajectories, one above it — a set
+# holds its own graph pools (the G network's saves over N x B rows, the actor's rollout saves), so
+# the second set costs 18 GB at lqr_var_d20's 16 384 trajectories on one GPU (45.4 vs 27.5 GB peak)
+# for 0.4 % of the iteration (22.06 vs 22.16 ms), while at 2 048 the copies it saves are a visible
+# part of a 3 ms iteration (profiles/r06_call5_pg_early_and_graph_sets.txt).  Both give bitwise the
+# same parameters (tests/test_gpu_training.py).
+_GS_ENV = os.environ.get("DPAC_GRAPH_SETS", "auto")
+GRAPH_SETS = _GS_ENV if _GS_ENV == "auto" else int(_GS_ENV)
+if GRAPH_SETS not in ("auto", 1, 2):
+    raise ValueError(f"DPAC_GRAPH_SETS must be auto, 1 or 2, got {_GS_ENV!r}")
+GRAPH_SETS_MAX_ROWS = 8192
+
+
+def graph_sets(rows: int) -> int:
+    """The graph sets train_iteration alternates for a rank batch of `rows` trajectories."""
+    if GRAPH_SETS == "auto":
+        return 2 if rows <= GRAPH_SETS_MAX_ROWS else 1
+    return GRAPH_SETS
 
 # DPAC_GUARD_DEFER=1 (default): the split graphs' backward chains (the actor's BPTT and its
 # parameter gradients, G's row backward and parameter gradients) launch their range-guard
@@ -622,7 +637,7 @@ class ActorCriticSolver(object):
         """The (critic, actor) samples of one training iteration (solver.py:67-70): the pair
         prefetch_samples() drew on a side stream if it matches, else drawn now.
 
-        With GRAPH_SETS = 2 the prefetched pair IS the static input of a captured graph set:
+        With two graph sets (graph_sets) the prefetched pair IS the static input of a set:
         the next prefetch_samples() into that set (two iterations later) overwrites it in
         place.  A caller that keeps a batch beyond its train_iteration must clone it."""
         spec = (num_sample, N_critic, N_actor)
@@ -649,7 +664,8 @@ class ActorCriticSolver(object):
         # the next iteration's graph set (train_iteration alternates two): its static inputs are
         # drawn into in place, once the iteration that last read them is done, so the next
         # iteration copies nothing in (round 5); otherwise fresh buffers
-        gset = self._gsets.get((num_sample, N_critic, N_actor)) if GRAPH_SETS == 2 else None
+        two = graph_sets(self.par.shard(num_sample)[1]) == 2
+        gset = self._gsets.get((num_sample, N_critic, N_actor)) if two else None
         gset = gset[self._parity] if gset else None
         with torch.cuda.stream(self._sample_side):
             if gset is not None:
@@ -906,7 +922,7 @@ class ActorCriticSolver(object):
         done = torch.cuda.Event()  # every reader of this set's static inputs is behind this point
         done.record()
         self._set_done[self._parity] = done
-        self._parity = (self._parity + 1) % GRAPH_SETS
+        self._parity = (self._parity + 1) % graph_sets(ccnt)
 
     def train_step_actor(self, train_data, total=None):
         g = self._grads("actor", lambda d: self.grad_actor(

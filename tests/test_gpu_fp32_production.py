@@ -201,7 +201,7 @@ def test_fp32_production_training_vs_oracle_vectors(path):
     # the split graphs (round 5: psol.GRAPH_SETS alternating sets, solver.train_iteration), and no
     # unsplit gradient graph
     sets = [s for v in sp._gsets.values() for s in v if s is not None]
-    assert len(sets) == psol.GRAPH_SETS and not sp._graphs
+    assert len(sets) == psol.graph_sets(batch) and not sp._graphs
     assert all(isinstance(a, psol._SplitActorGraphs) and isinstance(c, psol._SplitCriticGraphs) for a, c in sets)
     ref = g["history"]
     assert hist.shape == ref.shape

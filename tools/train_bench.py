@@ -75,7 +75,7 @@ def main():
                       "ms_per_iter": ms, "sequential_ms": (tc + ta) / a.iters * 1e3,
                       "critic_ms": tc / a.iters * 1e3, "actor_ms": ta / a.iters * 1e3,
                       "host_submit_ms": th / a.iters * 1e3,
-                      "traj_steps_per_s": 2 * B * N / (ms * 1e-3), "graph_sets": psol.GRAPH_SETS,
+                      "traj_steps_per_s": 2 * B * N / (ms * 1e-3), "graph_sets": psol.graph_sets(B),
                       "peak_allocated_GB": torch.cuda.max_memory_allocated() / 1e9,
                       "peak_reserved_GB": torch.cuda.max_memory_reserved() / 1e9}), flush=True)
 
