@@ -233,12 +233,39 @@ int pgw_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s, int ex
   return (int)hipGetLastError();
 }
 
+#ifndef DPAC_PGW_DEFAULT_D
+#define DPAC_PGW_DEFAULT_D 0  // k_param_grads_x3d by default (DPAC_PGW_KERNEL overrides)
+#endif
+// DPAC_PGW_KERNEL=w: the 16-wavefront merged-group kernel (k_param_grads_x3w, rounds 4-5); d: its
+// double-buffered 8-wavefront form (k_param_grads_x3d, round 6), bitwise the same results.
+inline bool pg_double() {
+  const char* e = getenv("DPAC_PGW_KERNEL");  // read per launch
+  return e ? e[0] == 'd' : DPAC_PGW_DEFAULT_D;
+}
+
+template <int NTI, bool L0 = false, int MODE = 0>
+int pgd_launch(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
+  using PL = PgdPlan<NTI, L0>;
+  auto k = k_param_grads_x3d<NTI, L0, MODE>;
+  if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, PL::kSmem))
+    return (int)e;
+  hipLaunchKernelGGL(k, dim3((unsigned)nch), dim3(kPgdThreads), PL::kSmem, s, a, l);
+  return (int)hipGetLastError();
+}
+
 // one layer of the split-fp16 kernel: the wide hidden layers and the input layer one 256-column
 // group of 16 waves (pgx_w_ok), other wide outputs 1 x 8 waves (one column tile each,
 // 128-column groups), outputs of <= 32 columns 8 x 1 waves over the row tiles
 int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   const int K = a.width[l], H = a.width[l + 1];
   const int nti = (K + 15) / 16;
+  if (pgx_w_ok(a, l) && pg_double()) {
+    if (l == 0) return nti <= 1 ? pgd_launch<1, true>(a, l, nch, s) : pgd_launch<2, true>(a, l, nch, s);
+    if (nti <= 4) return pgd_launch<4>(a, l, nch, s);
+    if (nti <= 8) return pgd_launch<8>(a, l, nch, s);
+    return pgd_launch<13>(a, l, nch, s);
+  }
   if (pgx_w_ok(a, l)) {
     if (l == 0) return nti <= 1 ? pgw_launch<1, true>(a, l, nch, s) : pgw_launch<2, true>(a, l, nch, s);
     if (nti <= 4) return pgw_launch<4>(a, l, nch, s);
@@ -291,7 +318,8 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
           if (nl >= 2) {
             const int64_t g = (nch + 7) / 8 * 8 * nl;
             if (int e = in ? pgw_launch<13, false, 2>(a, -(l + 8 * nl), g, s0, kPgwRawG0c)
-                           : pgw_launch<13, false, 1>(a, -(l + 8 * nl), g, s0))
+                           : (pg_double() ? pgd_launch<13, false, 1>(a, -(l + 8 * nl), g, s0)
+                                          : pgw_launch<13, false, 1>(a, -(l + 8 * nl), g, s0)))
               return e;
             l += nl - 1;
             continue;

@@ -714,4 +714,294 @@ __global__ __launch_bounds__(kPgwThreads) void k_param_grads_x3w(const PgArgs<fl
   if (bad) x3_flag(a.status);
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_param_grads_x3d (round 6): k_param_grads_x3w's sums, with the next
+// sub-chunk's loads in flight during this one's staging as well as its MFMAs.  x3w's 1 024-thread
+// workgroup has 128 VGPRs per lane and no LDS for a second raw block, so it issues the next loads
+// only after staging (measured: 3.7 TB/s of operand rows against 5.4 TB/s for the same row slices in
+// a plain streaming kernel, profiles/r05_call22_slice_bw.txt).  Here:
+//  * 8 wavefronts (512 threads, 256 VGPRs per lane), wave w owning the column tiles w and w + 8
+//    (NTI x 2 accumulator tiles), so each wave reads every A fragment for two column tiles and the
+//    A-image reads per sub-chunk halve;
+//  * G_{l+1} through registers and A's raw rows by LDS-DMA into two raw blocks: two stages (an
+//    unrolled pair of sub-chunks), each stage's loads issued as soon as its previous contents are
+//    consumed, so they are in flight through a whole sub-chunk; z_{l+1} (only the BN sums read it)
+//    by LDS-DMA into one raw block, issued once it is read (as x3w's), two phases ahead of use; the
+//    2^12 hi B operand is formed in registers (no third B image): 160 KiB of LDS at 13 tiles.
+// Arithmetic, order of every sum and partial layout are x3w's: bitwise its results.
+constexpr int kPgdThreads = 512;
+template <int NTI, bool L0 = false>
+struct PgdPlan {
+  static constexpr int KP = 16 * NTI;
+  static constexpr int kImgA = 2 * 4 * KP * 8 * 2;          // A hi, lo halves
+  static constexpr int kImgB = 2 * 4 * kPgwCW * 8 * 2;      // B hi, lo halves
+  static constexpr int kRaw = kPgxSR * kPgwCW * 4;          // one raw A block [32][256] floats
+  static constexpr int kRawA = kImgA + kImgB;               // two raw A blocks
+  static constexpr int kRawZ = kRawA + 2 * kRaw;            // one raw z_{l+1} block
+  static constexpr int kRawG0 = kRawZ + kRaw;               // L0: two compact G_0 blocks [32][32]
+  static constexpr int kCol = kRawG0 + (L0 ? 2 * kPgwRawG0c : 0);
+  static constexpr int kSmem = kCol + (4 * kPgwCW + 2 * kPgwCW) * 4;
+  static_assert(4 * 2 * kPgwCW * 4 + 4 * 2 * KP * 4 <= kRawA, "BN sums' reduction fits the image bytes");
+  static_assert(kSmem <= 160 * 1024, "LDS");
+};
+
+template <int NTI, bool L0 = false, int MODE = 0>
+__global__ __launch_bounds__(kPgdThreads) void k_param_grads_x3d(const PgArgs<float> a, const int lsel) {
+  using PL = PgdPlan<NTI, L0>;
+  constexpr int KP = PL::KP, CW = kPgwCW;
+  static_assert(MODE == 0 || !L0, "merged launches hold wide layers only");
+  static_assert(!L0 || KP <= 32, "the input layer: K <= 32");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // PL::kSmem bytes (dynamic)
+  _Float16* const sA = reinterpret_cast<_Float16*>(smem);
+  _Float16* const sB = reinterpret_cast<_Float16*>(smem + PL::kImgA);
+  float* const s_cmax = reinterpret_cast<float*>(smem + PL::kCol);
+  float* const s_cfac = s_cmax + 4 * CW;
+  int* const s_cexp = reinterpret_cast<int*>(s_cfac + CW);
+  if (x3_status_set(a.status)) return;  // fell back: the f32 kernel after this one does the work
+  const int64_t bx = blockIdx.x;
+  const int nl = MODE == 0 ? 1 : (-lsel) >> 3;
+  const int l = MODE == 0 ? lsel : ((-lsel) & 7) + (int)((bx >> 3) % nl);
+  const int64_t chunk = MODE == 0 ? bx : (bx / (8 * nl)) * 8 + (bx & 7);
+  if (chunk * a.rows_per_chunk >= a.rows) return;  // past the last chunk (merged grid), before any barrier
+  bool bad = false;
+  const int K = a.width[l], H = a.width[l + 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // column tiles wave, wave + 8
+  const int rb = tid >> 7, fl = tid & 127;                     // staging: 8-row block; features / columns fl, fl + 128
+  const int rbu = __builtin_amdgcn_readfirstlane(rb);
+  const int64_t r_begin = chunk * a.rows_per_chunk;
+  const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
+  const bool last = l == a.L;
+  const float* srcA = L0 ? a.x : a.z + a.zoff[l];
+  const int64_t ldA = L0 ? a.ldx : a.ztot;
+  const float* gB = a.G + a.goff[l + 1];
+  const float* zB = a.z + a.zoff[l + 1];
+  float sa[2], ha[2], sbv[2], bbv[2], csb_b[2], csb_s[2];
+  uint32_t offB[2];
+  bool fa[2];
+  int cexp[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = fl + 128 * h;
+    fa[h] = k < K;
+    sa[h] = fa[h] ? a.scale[l][k] : 0.f;
+    ha[h] = fa[h] ? a.shift[l][k] : 0.f;
+    const bool fb = k < H;
+    sbv[h] = fb ? a.scale[l + 1][k] : 0.f;
+    bbv[h] = (fb && last) ? a.bias[k] : 0.f;
+    offB[h] = fb ? (uint32_t)k * 4u : kOOB;
+    csb_b[h] = csb_s[h] = 0.f;
+    cexp[h] = -100;
+  }
+  float cs0_b = 0.f, cs0_s = 0.f;  // L0: BN_0's sums, feature fl
+  pgf4 acc[NTI][2];  // 2^12 x (the column-scaled) dW tiles: features 16 t + 4 fq .., columns 16 (wave + 8 j) + fi
+#pragma unroll
+  for (int t = 0; t < NTI; ++t) acc[t][0] = acc[t][1] = pgf4{0.f, 0.f, 0.f, 0.f};
+  float gst[2][2][8];  // [stage][h][row]: G_{l+1} at rows 8 rb + i, columns fl + 128 h
+  const uint32_t voffA = pgw_lane_off((uint32_t)K * 4u, lane), voffZ = pgw_lane_off((uint32_t)H * 4u, lane);
+  const float* const rawZ = reinterpret_cast<const float*>(smem + PL::kRawZ);
+
+  // z_{l+1}'s 32 rows at r0 into the raw z block, wave w copying rows 4 w .. 4 w + 3 (past the
+  // chunk: its last row again; times G = 0 it adds nothing)
+  auto issue_z = [&](int64_t r0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * wave + j;
+      pgw_row_dma(zB + min(r0 + i, r_end - 1) * a.ztot, voffZ, smem + PL::kRawZ + i * CW * 4);
+    }
+  };
+  // the 32 rows at r0 into stage S: G rows through registers, then the raw A rows (and G_0 rows)
+  // by LDS-DMA, wave w copying rows 4 w .. 4 w + 3.  Rows past the chunk: G reads 0, the DMA
+  // repeats the chunk's last row.
+  auto issue = [&](int64_t r0, auto sidx) {
+    constexpr int S = decltype(sidx)::value;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t row = r0 + 8 * rbu + i;
+      const auto rB = make_rsrc(gB + row * a.gtot, row < r_end ? (uint32_t)H * 4u : 0u);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) gst[S][h][i] = buf_load_elem<float>(rB, offB[h]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * wave + j;
+      const int64_t row = min(r0 + i, r_end - 1);
+      pgw_row_dma(srcA + row * ldA, voffA, smem + PL::kRawA + S * PL::kRaw + i * CW * 4);
+      if constexpr (L0)
+        pgw_row_dma_128(a.G + a.goff[0] + row * a.gtot, (uint32_t)K * 4u, lane,
+                        smem + PL::kRawG0 + S * kPgwRawG0c + i * 128);
+    }
+  };
+  constexpr int kIssueOps = 16 + 4 * (L0 ? 2 : 1);  // vector memory instructions per wave and issue
+
+  const int fq = lane >> 4, fi = lane & 15;
+  const _Float16* const aBase = sA + (fq * KP + fi) * 8;  // + (part 4 KP + 16 t) 8
+  auto sub = [&](int64_t r0, auto sidx) {
+    constexpr int S = decltype(sidx)::value;
+    const float* const rawA = reinterpret_cast<const float*>(smem + PL::kRawA + S * PL::kRaw);
+    const float* const rawG0 = reinterpret_cast<const float*>(smem + PL::kRawG0 + S * kPgwRawG0c);
+    // this sub-chunk's rows have landed once only the issue made right after its z rows is
+    // outstanding: issues come in the order (G, A)_k .. z_k, (G, A)_{k+1}, so that is the next
+    // sub-chunk's (if any)
+    if (r0 + kPgxSR < r_end) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kIssueOps) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // raw rows in LDS; the previous sub-chunk's fragment reads are done
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // A: features fl + 128 h of rows 8 rb .. + 7, BN and the activation, split
+      const int k = fl + 128 * h;
+      if (h == 1 && 128 >= KP) continue;  // compile-time: no second feature
+      if (k < KP) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float xv = rawA[(8 * rb + i) * CW + k];
+          const float y = ha[h] + xv * sa[h];
+          if constexpr (L0) {  // BN_0 only (solver.py:260-262); its sums over the chunk's rows
+            v[i] = fa[h] ? y : 0.f;
+            if (fa[h] && r0 + 8 * rb + i < r_end) {
+              const float g0 = rawG0[(8 * rb + i) * 32 + k];
+              cs0_b += g0;
+              cs0_s += g0 * xv;
+            }
+          } else {
+            v[i] = fa[h] ? y + fmaxf(y, 0.f) : 0.f;  // hidden activations
+          }
+        }
+        pgh8 hh, lo;
+        pgx_split8(v, hh, lo);
+        bad |= x3_bad4(v[0], v[1], v[2], v[3]) | x3_bad4(v[4], v[5], v[6], v[7]);
+        *reinterpret_cast<pgh8*>(sA + ((0 * 4 + rb) * KP + k) * 8) = hh;
+        *reinterpret_cast<pgh8*>(sA + ((1 * 4 + rb) * KP + k) * 8) = lo;
+      }
+    }
+    float vb[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // B: columns fl + 128 h, their sums and the sub-chunk's column max
+      float m = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float gv = gst[S][h][i];
+        vb[h][i] = gv * sbv[h];
+        m = fmaxf(m, fabsf(vb[h][i]));
+        csb_b[h] += gv;
+        csb_s[h] += gv * (rawZ[(8 * rb + i) * CW + fl + 128 * h] + bbv[h]);  // bbv = 0 unless the output layer
+      }
+      s_cmax[rb * CW + fl + 128 * h] = m;
+    }
+    __syncthreads();  // the column maxima; every raw row of this stage read
+    if (r0 + kPgxSR < r_end) issue_z(r0 + kPgxSR);              // the raw z block is free: the next sub-chunk's
+    if (r0 + 2 * kPgxSR < r_end) issue(r0 + 2 * kPgxSR, sidx);  // this stage is free: two sub-chunks ahead
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = fl + 128 * h;
+      const float m = fmaxf(fmaxf(s_cmax[c], s_cmax[CW + c]), fmaxf(s_cmax[2 * CW + c], s_cmax[3 * CW + c]));
+      int e = cexp[h];
+      if (m > 0.f && m < 3.0e38f) {
+        int em = 0;
+        (void)frexpf(m, &em);
+        e = em > cexp[h] ? em : cexp[h];
+      }
+      const float sc = ldexpf(1.f, 3 - e);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vb[h][i] *= sc;
+      pgh8 hh, lo;
+      pgx_split8(vb[h], hh, lo);
+      bad |= x3_bad4(vb[h][0], vb[h][1], vb[h][2], vb[h][3]) | x3_bad4(vb[h][4], vb[h][5], vb[h][6], vb[h][7]);
+      *reinterpret_cast<pgh8*>(sB + ((0 * 4 + rb) * CW + c) * 8) = hh;
+      *reinterpret_cast<pgh8*>(sB + ((1 * 4 + rb) * CW + c) * 8) = lo;
+      if (rb == 0) {
+        s_cfac[c] = ldexpf(1.f, cexp[h] - e);
+        s_cexp[c] = e;
+      }
+      cexp[h] = e;
+    }
+    __syncthreads();  // the images
+    pgh8 bh[2], bl[2], b12[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cT = (wave + 8 * j) * 16 + fi;
+      bh[j] = *reinterpret_cast<const pgh8*>(sB + (fq * CW + cT) * 8);
+      bl[j] = *reinterpret_cast<const pgh8*>(sB + ((4 + fq) * CW + cT) * 8);
+      b12[j] = bh[j] * (_Float16)kPgxLo;  // exact: |hi| < 8
+      const float f = s_cfac[cT];
+      if (__any(f != 1.f)) {
+#pragma unroll
+        for (int t = 0; t < NTI; ++t) acc[t][j] *= f;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NTI; ++t) {
+      const pgh8 xh = *reinterpret_cast<const pgh8*>(aBase + 16 * t * 8);
+      const pgh8 xl = *reinterpret_cast<const pgh8*>(aBase + (4 * KP + 16 * t) * 8);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, b12[j], acc[t][j], 0, 0, 0);
+        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, bl[j], acc[t][j], 0, 0, 0);
+        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, bh[j], acc[t][j], 0, 0, 0);
+      }
+    }
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  issue(r_begin, S0{});
+  issue_z(r_begin);
+  if (r_begin + kPgxSR < r_end) issue(r_begin + kPgxSR, S1{});
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * kPgxSR) {
+    sub(r0, S0{});
+    if (r0 + kPgxSR < r_end) sub(r0 + kPgxSR, S1{});
+  }
+
+  // ---- this chunk's partial dW_l: lane holds features 16 t + 4 fq .. +3, columns cT_j ----
+  float* part = a.part + chunk * a.ptot;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int cT = (wave + 8 * j) * 16 + fi;
+    const float us = ldexpf(1.f, s_cexp[cT] - 3 - 12);  // undo 2^12 and the column scale
+#pragma unroll
+    for (int t = 0; t < NTI; ++t) {
+      const pgf4 c = acc[t][j] * us;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int k = 16 * t + 4 * fq + v;
+        if (k < K && cT < H) part[a.off_W[l] + (int64_t)k * H + cT] = c[v];
+      }
+    }
+  }
+  // ---- BN column sums: combine the 4 row blocks through LDS (reusing the images) ----
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    red[(rb * 2 + 0) * CW + fl + 128 * h] = csb_b[h];
+    red[(rb * 2 + 1) * CW + fl + 128 * h] = csb_s[h];
+  }
+  float* red0 = red + 4 * 2 * CW;  // L0: [4 rb][2][KP]
+  if (L0 && fl < KP) {
+    red0[(rb * 2 + 0) * KP + fl] = cs0_b;
+    red0[(rb * 2 + 1) * KP + fl] = cs0_s;
+  }
+  __syncthreads();
+  if (L0 && tid < K) {
+    float sb = 0.f, ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sb += red0[(w * 2 + 0) * KP + tid];
+      ss += red0[(w * 2 + 1) * KP + tid];
+    }
+    part[a.off_beta[0] + tid] = sb;
+    part[a.off_gamma[0] + tid] = ss;
+  }
+  if (tid < CW && tid < H) {
+    float sb = 0.f, ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sb += red[(w * 2 + 0) * CW + tid];
+      ss += red[(w * 2 + 1) * CW + tid];
+    }
+    part[a.off_beta[l + 1] + tid] = sb;
+    part[a.off_gamma[l + 1] + tid] = ss;
+  }
+  if (bad) x3_flag(a.status);
+}
+
 }  // namespace dpac

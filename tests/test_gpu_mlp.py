@@ -138,12 +138,16 @@ def test_param_grads_split_fp16_vs_torch(widths, R, gscale, monkeypatch):
     ((12, 52, 100, 36, 8), 1234),          # 4- and 7-tile inputs, 100- and 36-column outputs
     ((8, 64, 40, 12), 999)])               # a one-tile input layer, a 12-column output layer
 @pytest.mark.parametrize("gscale", [1.0, "ramp"])
-def test_param_grads_merged_group_kernel_bitwise(widths, R, gscale, monkeypatch):
+@pytest.mark.parametrize("kern", ["w", "d"])
+def test_param_grads_merged_group_kernel_bitwise(widths, R, gscale, kern, monkeypatch):
     """The merged-group split-fp16 kernel (k_param_grads_x3w: one 256-column group, operand
     rows by LDS-DMA; for the input layer, the hidden layers with more than 32 inputs and the
     narrow output layer) forms the same products in the same order as the earlier kernels
     (DPAC_PGX_W=0: two 128-column groups, or 8 waves over the row tiles for <= 32 columns): the
-    gradients, BN_0's sums included, are bitwise equal, column rescaling included (ramp)."""
+    gradients, BN_0's sums included, are bitwise equal, column rescaling included (ramp).
+    kern (DPAC_PGW_KERNEL): the 16-wavefront kernel (w) or its double-buffered 8-wavefront form
+    k_param_grads_x3d (d, round 6), which must also equal w bit for bit."""
+    monkeypatch.setenv("DPAC_PGW_KERNEL", kern)
     scales, shifts, Ws, b = random_net(widths, torch.float32, seed=3 * R + len(widths))
     g = torch.Generator().manual_seed(R + 1)
     rnd = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(torch.float32).to(DEV)
@@ -169,9 +173,16 @@ def test_param_grads_merged_group_kernel_bitwise(widths, R, gscale, monkeypatch)
     for a, c in zip(merged, two):
         assert torch.isfinite(a).all()
         assert torch.equal(a, c), float((a - c).abs().max())
+    monkeypatch.delenv("DPAC_PG_X3")
+    monkeypatch.delenv("DPAC_PGX_W")
+    monkeypatch.setenv("DPAC_PGW_KERNEL", "d" if kern == "w" else "w")
+    other = ops.mlp_param_grads(view, x, z, G, like)
+    for a, c in zip(merged, other):
+        assert torch.equal(a, c), float((a - c).abs().max())
 
 
-def test_param_grads_merged_group_high_address_words(monkeypatch):
+@pytest.mark.parametrize("kern", ["w", "d"])
+def test_param_grads_merged_group_high_address_words(kern, monkeypatch):
     """Regression test of round 4's address fault in k_param_grads_x3w (the operand rows'
     global_load_lds_dwordx4 takes a wave-uniform row address built from two readfirstlane
     halves; its first build sign-extended the low word, so any row whose address had bit 31
@@ -181,7 +192,9 @@ def test_param_grads_merged_group_high_address_words(monkeypatch):
     boundary, so its rows have low words just below 2^32 and then just above 0 with the high
     word carried.  The gradients must equal, bit for bit, those of the same kernel on
     ordinarily placed copies and those of the two-group kernels (DPAC_PGX_W=0), and lie within
-    the split-fp16 tolerance of the exact-f32 kernel."""
+    the split-fp16 tolerance of the exact-f32 kernel.  kern: DPAC_PGW_KERNEL (w, or d: round 6's
+    double-buffered k_param_grads_x3d, whose z rows also move by LDS-DMA)."""
+    monkeypatch.setenv("DPAC_PGW_KERNEL", kern)
     widths, R = (20, 200, 200, 200, 20), 20000
     scales, shifts, Ws, b = random_net(widths, torch.float32, seed=4242)
     g = torch.Generator().manual_seed(4243)
