@@ -27,7 +27,7 @@ EQN_OBJS  := $(foreach e,$(EQNS),$(foreach d,$(call eqn_dims,$(e)),$(foreach t,f
 OBJS      := $(OBJDIR)/dpac_abi.o $(OBJDIR)/dpac_mlp.o $(OBJDIR)/dpac_params.o $(EQN_OBJS)
 LIB       := $(PKG)/libdpac.so
 
-.PHONY: all lib ext bounds clean
+.PHONY: all lib ext plugins bounds clean
 all: lib
 lib: $(LIB)
 
@@ -73,12 +73,15 @@ $(EXTDIR)/dpac_eqn_$(1)_$(2)_d$(3).o: $(CSRC)/dpac_eqn_$(1).hip
 endef
 $(foreach d,$(EXT_LIST),$(foreach e,$(call ext_eqns,$(d)),$(foreach t,f32 f64,$(eval $(call EXT_RULE,$(e),$(t),$(d))))))
 define EXT_LIB
-$(PKG)/libdpac_d$(1).so: $(call ext_objs,$(1)) $(LIB)
+$(PKG)/libdpac_d$(1).so: $(call ext_objs,$(1))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $$@ $(call ext_objs,$(1)) -L$(PKG) -ldpac -Wl,-rpath,'$$$$ORIGIN'
 endef
 $(foreach d,$(EXT_LIST),$(eval $(call EXT_LIB,$(d))))
 -include $(wildcard $(EXTDIR)/*.d)
-ext: $(foreach d,$(EXT_LIST),$(PKG)/libdpac_d$(d).so)
+ext: lib $(foreach d,$(EXT_LIST),$(PKG)/libdpac_d$(d).so)
+# the plugins alone, against the libdpac.so in place (never rebuilt here): _lib.ensure_dim's
+# on-demand build, which must not relink a library the calling process has loaded
+plugins: $(foreach d,$(EXT_LIST),$(PKG)/libdpac_d$(d).so)
 
 clean:
 	rm -rf build $(LIB) $(PKG)/libdpac_d*.so

@@ -547,6 +547,7 @@ class ActorCriticSolver(object):
             raise _lib.DpacUnavailable("ActorCriticSolver needs a ROCm GPU (libdpac has no CPU path)")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         _lib.load()
+        _lib.ensure_dim(bsde.params())  # a dimension outside the main build: its plugin, built on demand
         self.par = parallel or SingleProcess()
         # one seed for every rank: the Philox stream is keyed by global trajectory index,
         # so the shards of a batch are its rows whatever the world size

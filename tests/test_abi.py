@@ -242,3 +242,29 @@ def test_dimension_plugin_registers_d7():
     with pytest.raises(_lib.DpacError) as ei:
         _lib.call("dpac_flag_init", ctypes.byref(p9), _lib.SCHEME_ADAPTIVE, _lib.F64, 4, 10, 0.2, None, None, None)
     assert ei.value.code == _lib.DPAC_EUNSUP and "make ext" in str(ei.value)
+
+
+def test_ensure_dim_builds_the_plugin_on_demand(monkeypatch, tmp_path):
+    """Round 6: a solver meeting a dimension without kernels has its plugin
+    compiled on demand (`make ext EXT_DIMS=<d>`, under a lock file so data-parallel ranks build it
+    once) and loaded; DPAC_AUTO_PLUGIN=0 (auto=False) leaves it unsupported, and dimensions above
+    MAX_PLUGIN_DIM are refused.  Host-side: the build command is captured, not run."""
+    import subprocess
+    from deeppde_actorcritic_amd import equation as peq
+    from tests.helpers import full_config
+    built = []
+
+    class FakeLib:
+        def dpac_supported(self, eq_ref):
+            return 1 if built else 0
+    monkeypatch.setattr(_lib, "load", lambda: FakeLib())
+    monkeypatch.setattr(_lib, "_load_new_plugins", lambda: FakeLib())
+    monkeypatch.setattr(subprocess, "run", lambda cmd, check: built.append(cmd))
+    p9 = peq.LQR(full_config("LQR", 9).eqn_config).params()
+    assert _lib.ensure_dim(p9, auto=False) is False and not built
+    assert _lib.ensure_dim(p9, auto=True) is True
+    assert len(built) == 1 and built[0][-2:] == ["plugins", "EXT_DIMS=9"]
+    assert _lib.ensure_dim(p9, auto=True) is True and len(built) == 1  # supported now: no rebuild
+    built.clear()
+    p40 = peq.LQR(full_config("LQR", 40).eqn_config).params()
+    assert _lib.ensure_dim(p40, auto=True) is False and not built

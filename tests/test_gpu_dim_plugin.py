@@ -6,7 +6,11 @@ libdpac_d7.so, whose instantiations register into libdpac's dispatch table when 
 loads it.  Checked at d = 7 against the float64 oracle: the rollout of both schemes for the
 three equations that allow an odd dimension (VDP needs d = 2c), and joint actor-critic training
 (solver.py:36-71), at the tolerances of the d = 20 tests (1e-12 paths, 1e-8 training).
+DPAC_TEST_DIM=<d> runs the same checks at another dimension: without a prebuilt plugin the
+first call builds it on demand (_lib.ensure_dim, round 6: a run-time state dimension).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -20,7 +24,7 @@ from tests.helpers import full_config, rel_close
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-D = 7
+D = int(os.environ.get("DPAC_TEST_DIM", "7"))
 
 
 @pytest.mark.parametrize("scheme", ["adaptive", "naive"])
@@ -28,6 +32,7 @@ D = 7
 def test_rollout_d7_matches_oracle(name, scheme):
     cfg = full_config(name, D, N=16, scheme=scheme)
     bp, bo = getattr(peq, name)(cfg.eqn_config), oeq.make(cfg.eqn_config)
+    assert _lib.ensure_dim(bp.params())  # prebuilt (d = 7) or compiled on demand
     assert _lib.load().dpac_supported(bp.params()) == 1
     np.random.seed(3)
     B, N = 300, 16
