@@ -200,8 +200,8 @@ __global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int64_t b0, int nb
                                                    uint64_t seed, int64_t traj_offset, T* dw) {
   // thread (unit u, trajectory b0 + bl, lane slot p, block): the stream layout of draw_slot(); a
   // unit is a step pair in the paired layout (S = 2), else one step.  x runs over this launch's
-  // (bl, p, block) in 32-bit arithmetic, y over the units (round 6: one 64-bit division chain per
-  // block cost more than its Philox rounds)
+  // (bl, p, block) in 32-bit arithmetic, y over the units with a stride (round 6: the index
+  // divisions formed once per thread, not per block: they cost more than its Philox rounds)
   const int P = lanes_for_dim(D), M = comps_per_lane(D);
   const int PB = dw_per_block<T>(sample_type);
   const int S = dw_steps_per_block<T>(M, sample_type);
@@ -215,17 +215,41 @@ __global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int64_t b0, int nb
   const int p = (int)rem / BPU, blk = (int)rem - p * BPU;
   const int64_t b = b0 + bl;
   const uint64_t traj = (uint64_t)(traj_offset + b);
-  for (int u = blockIdx.y; u < units; u += gridDim.y) {
+  // the values' places, fixed per thread: step offset within the unit and component (-1: none)
+  int toff[4], jj[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int iv = blk * PB + e;  // the value's place in the lane slot's unit
+    const int m = S == 2 ? iv % M : iv;
+    const bool ok = e < PB && (S == 2 ? iv < 2 * M : m < M) && p * M + m < D;
+    toff[e] = S == 2 ? iv / M : 0;
+    jj[e] = ok ? p * M + m : -1;
+  }
+  T* const dwb = dw + b * D;
+  const int64_t step = B * D;
+  // two components per lane slot and step, d even, four values a block (f32 d = 20): each step's
+  // pair is one 8-byte store
+  if constexpr (sizeof(T) == 4) {
+    if (S == 2 && M == 2 && PB == 4 && (D & 1) == 0) {
+      if (jj[0] < 0) return;
+      for (int u = blockIdx.y; u < units; u += gridDim.y) {
+        T vals[4];
+        dw_block_values<T>(seed, traj, (uint64_t)u * P + p, sample_type, vals);
+        const int t = 2 * u;
+        *reinterpret_cast<float2*>(dwb + (int64_t)t * step + jj[0]) = make_float2(vals[0], vals[1]);
+        if (t + 1 < N)
+          *reinterpret_cast<float2*>(dwb + (int64_t)(t + 1) * step + jj[0]) = make_float2(vals[2], vals[3]);
+      }
+      return;
+    }
+  }
+  for (int u = blockIdx.y; u < units; u += gridDim.y) {  // a few units per thread (grid y ~ 16)
     T vals[4];
     dw_block_values<T>(seed, traj, ((uint64_t)u * P + p) * BPU + blk, sample_type, vals);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      if (e >= PB) break;
-      const int iv = blk * PB + e;  // the value's place in the lane slot's unit
-      const int t = S == 2 ? 2 * u + iv / M : u;
-      const int m = S == 2 ? iv % M : iv;
-      const int j = p * M + m;
-      if ((S == 2 ? iv < 2 * M : m < M) && t < N && j < D) dw[((int64_t)t * B + b) * D + j] = vals[e];
+      const int t = (S == 2 ? 2 * u : u) + toff[e];
+      if (jj[e] >= 0 && t < N) dwb[(int64_t)t * step + jj[e]] = vals[e];
     }
   }
 }
@@ -284,6 +308,61 @@ __global__ __launch_bounds__(256) void k_sample_points(int64_t B, int D, double 
     dir_write<T>(seed, traj, kTagBdry, D, Rt, sqrt(dir_sumsq<T>(seed, traj, kTagBdry, D)), x_bdry + b * D);
 }
 
+// One group of G = pow2 >= ceil(D / PB) lanes per (trajectory, point): lane c draws block c of
+// the direction, lane 0 folds the squares in component order through shuffles (the same sum, bit
+// for bit, as dir_sumsq), and every lane writes its block's components (round 6: the one-thread-
+// per-trajectory kernel ran 16 workgroups at B = 4096, 10 us for 0.6 MB).  Point 0 is x0, 1 x_bdry.
+template <typename T>
+__global__ __launch_bounds__(256) void k_sample_points_grouped(int64_t B, int D, int G, double R,
+                                                               int sample_type, uint64_t seed,
+                                                               int64_t traj_offset, T* x0, T* x_bdry) {
+  constexpr int PB = Rng<T>::kNormalPerBlock;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (int)(idx & (G - 1));
+  const int64_t task = idx / G;
+  const int64_t b = task >> 1;
+  const int kind = (int)(task & 1);
+  T* const out = kind == 0 ? x0 : x_bdry;
+  if (b >= B || out == nullptr) return;  // whole groups: G divides 64 and the grid
+  const T Rt = (T)R;
+  if (kind == 0 && sample_type == DPAC_SAMPLE_ZERO_X0) {
+    for (int j = c; j < D; j += G) x0[b * D + j] = (T)0.01;  // np.zeros + 0.01 (:39)
+    return;
+  }
+  const uint64_t traj = (uint64_t)(traj_offset + b);
+  const uint64_t tag = kind == 0 ? kTagDir : kTagBdry;
+  const int nblk = (D + PB - 1) / PB;
+  T n[PB];
+  if (c < nblk) {
+    Rng<T>::normals(philox_block(seed, traj, (tag << 48) | (uint64_t)c), n);
+  } else {
+#pragma unroll
+    for (int e = 0; e < PB; ++e) n[e] = 0;
+  }
+  T ss = 0;
+  for (int k = 0; k < nblk; ++k) {
+#pragma unroll
+    for (int e = 0; e < PB; ++e) {
+      const T v = __shfl(n[e], k, G);
+      if (k * PB + e < D) ss += v * v;
+    }
+  }
+  const T nrm = sqrt(__shfl(ss, 0, G));
+  T scale = Rt;
+  if (kind == 0) {  // r = (R*U)^(1/d) * R^((d-1)/d), U uniform (0,1]  (:14-15)
+    const uint4 v = philox_block(seed, traj, kTagRadius << 48);
+    T U;
+    if constexpr (sizeof(T) == 4) U = rocrand_device::detail::uniform_distribution(v.x);
+    else U = rocrand_device::detail::uniform_distribution_double(v.x, v.y);
+    scale = pow(Rt * U, (T)1 / (T)D) * pow(Rt, (T)(D - 1) / (T)D);
+  }
+  if (c < nblk) {
+#pragma unroll
+    for (int e = 0; e < PB; ++e)
+      if (c * PB + e < D) out[b * D + c * PB + e] = (scale * n[e]) / nrm;
+  }
+}
+
 template <typename T>
 int sample_impl(const dpac_eqn_params* eq, int32_t sample_type, int64_t B, int32_t N,
                 uint64_t seed, int64_t off, void* x0, void* dw, void* x_bdry, hipStream_t s) {
@@ -297,15 +376,28 @@ int sample_impl(const dpac_eqn_params* eq, int32_t sample_type, int64_t B, int32
     const int64_t chunk = (int64_t)1 << 24;  // trajectories per launch: 32-bit thread indices
     for (int64_t b0 = 0; b0 < B; b0 += chunk) {
       const int nb = (int)std::min<int64_t>(chunk, B - b0);
-      const dim3 g((unsigned)(((int64_t)nb * per_b + 255) / 256), (unsigned)std::min(units, 65535));
+      // y: a few units per thread, more when x alone would not fill the chip
+      const int64_t gx = ((int64_t)nb * per_b + 255) / 256;
+      const int gy = (int)std::min<int64_t>(units, std::max<int64_t>(16, (4096 + gx - 1) / gx));
+      const dim3 g((unsigned)gx, (unsigned)gy);
       hipLaunchKernelGGL(k_sample_dw<T>, g, dim3(256), 0, s, B, b0, nb, N, D, st, seed, off, (T*)dw);
       if (hipError_t e = hipGetLastError()) return (int)e;
     }
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
   if (x0 || x_bdry) {
-    hipLaunchKernelGGL(k_sample_points<T>, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B,
-                       D, eq->R, sample_type, seed, off, (T*)x0, (T*)x_bdry);
+    const int nblk = (D + Rng<T>::kNormalPerBlock - 1) / Rng<T>::kNormalPerBlock;
+    int G = 1;
+    while (G < nblk) G *= 2;
+    const char* serial = getenv("DPAC_SAMPLE_POINTS_SERIAL");  // read per call: tests compare the two
+    if (G <= 64 && !(serial && serial[0] == '1')) {
+      const int64_t threads = 2 * B * G;
+      hipLaunchKernelGGL(k_sample_points_grouped<T>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                         B, D, G, eq->R, sample_type, seed, off, (T*)x0, (T*)x_bdry);
+    } else {  // more than 64 blocks of a direction: one thread per trajectory
+      hipLaunchKernelGGL(k_sample_points<T>, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, B,
+                         D, eq->R, sample_type, seed, off, (T*)x0, (T*)x_bdry);
+    }
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
   return 0;

@@ -203,6 +203,35 @@ def test_sampler_distribution_and_sharding(dtype):
     assert torch.all(x00 == torch.tensor(0.01, dtype=dtype))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("d", [1, 3, 5, 20, 33, 200])
+@pytest.mark.parametrize("sample_type", [_lib.SAMPLE_NORMAL, _lib.SAMPLE_ZERO_X0])
+def test_grouped_point_sampler_equals_one_thread_per_trajectory(d, dtype, sample_type):
+    """Round 6: x0 and x_bdry drawn by one lane group per (trajectory, point), the squares folded
+    in component order through shuffles, equal bit for bit the one-thread-per-trajectory kernel
+    (DPAC_SAMPLE_POINTS_SERIAL=1; the path directions of more than 64 counter blocks take), for
+    dimensions that leave partial blocks and idle lanes in the group."""
+    eqp = pe(eqn_config("LQR", 20)).params()
+    eqp.dim = d
+    out = {}
+    old = os.environ.get("DPAC_SAMPLE_POINTS_SERIAL")
+    try:
+        for k in ("0", "1"):
+            os.environ["DPAC_SAMPLE_POINTS_SERIAL"] = k
+            out[k] = ops.sample(eqp, sample_type, 1001, 1, seed=19, traj_offset=7, dtype=dtype, device=DEV,
+                                want_dw=False)
+    finally:
+        if old is None:
+            os.environ.pop("DPAC_SAMPLE_POINTS_SERIAL", None)
+        else:
+            os.environ["DPAC_SAMPLE_POINTS_SERIAL"] = old
+    for a, b in zip(out["0"], out["1"]):
+        if a is not None:
+            assert torch.equal(a, b)
+    nb = torch.linalg.norm(out["0"][2].double(), dim=1)
+    assert torch.allclose(nb, torch.full_like(nb, float(eqp.R)), rtol=1e-5 if dtype == torch.float32 else 1e-13)
+
+
 @pytest.mark.parametrize("N", [64, 63])
 @pytest.mark.parametrize("name,d", [("LQR", 20), ("LQR", 5), ("VDP", 20), ("EKN", 10)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
@@ -337,7 +366,7 @@ def test_sampler_stream_is_a_function_of_step_and_component(dtype, sample_type):
                                         ("LQR_var", 10, 33, 101), ("LQR", 5, 37, 13), ("VDP", 20, 70, 30)])
 def test_inkernel_philox_generator_rollout_bitwise(name, d, B, N, scheme, sample_type):
     """Round 6: the in-kernel Philox rollout with the increments drawn by
-    generator wavefronts into the staged kernel's LDS ring (k_rollout_staged<..., GEN = 4>, the
+    generator wavefronts into the staged kernel's LDS ring (k_rollout_staged<..., GEN = 12>, the
     default for float) gives bitwise the results of k_rollout drawing them in each compute lane
     (DPAC_ROLLOUT_STAGED=0): odd horizons (a last unpaired step), partial workgroups, chunks that
     wrap the ring, the u and cost outputs (VDP and float64 keep k_rollout)."""

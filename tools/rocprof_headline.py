@@ -5,7 +5,7 @@ next to the bench line the same command printed:
     rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o run --output-format csv -- \\
         python bench.py --steps 20 --warmup 5 > gpurun_out/prof_kt.log
     python tools/rocprof_headline.py gpurun_out/prof_kt/run_kernel_trace.csv gpurun_out/prof_kt.log \\
-        --steps 20 --warmup 5 > profiles/r04_rocprof_headline.json
+        --steps 20 --warmup 5 > profiles/r06_rocprof_headline.json
 
 bench.py launches dpac::k_rollout_staged<float, ...> (f32, LQR d = 20, no cost / u outputs) in
 this order: W warm-up + K timed launches over the 5 cold sets, then (only with --mall) 5
