@@ -74,7 +74,7 @@ def main(tag):
         return
     # canonical rollout: f32, LQR d=20 (16 lanes/trajectory), adaptive, dw from HBM, no cost/u outputs
     # (the LDS-staged kernel k_rollout_staged; k_rollout takes Philox / unstaged shapes)
-    key_kernel = "k_rollout_staged<float, dpac::EqLQR<float, 20, 16>, 20, 1, 0,"
+    key_kernel = "k_rollout_staged<float, dpac::EqLQR<float, 20, 16>, 20, 1, 0, 8, 0>"  # GEN = 0: dw from HBM
     fetch_kib, nf, row = counter_mean(f, key_kernel, "FETCH_SIZE")
     write_kib, nw, _ = counter_mean(w, key_kernel, "WRITE_SIZE")
     fetch_b = fetch_kib * 1024 * 2  # gfx950: FETCH_SIZE counts 64 B per 128-B request
