@@ -290,6 +290,55 @@ int launch_x3_layer(const PgArgs<float>& a, int l, int64_t nch, hipStream_t s) {
   return pgx_launch<13, 1, 1, false>(a, l, grid, s);
 }
 
+// The configuration launch_x3_layer gives layer l off the merged-group kernels (pgx_w_ok false)
+// and its column groups, as a k_param_grads_x3_seg segment
+inline int x3_layer_cfg(const PgArgs<float>& a, int l, int& ngrp) {
+  const int K = a.width[l], H = a.width[l + 1];
+  const int nti = (K + 15) / 16;
+  if (H <= 32) {
+    const int ntj = (H + 15) / 16, nt8 = (nti + 7) / 8;
+    ngrp = 1;
+    if (nt8 <= 1) return ntj == 1 ? kPgxN11 : kPgxN12;
+    return ntj == 1 ? kPgxN21 : kPgxN22;
+  }
+  ngrp = (H + 127) / 128;
+  if (l == 0) return nti <= 1 ? kPgxIn1 : kPgxIn2;
+  if (nti <= 1) return kPgxW1;
+  if (nti <= 2) return kPgxW2;
+  if (nti <= 4) return kPgxW4;
+  if (nti <= 8) return kPgxW8;
+  return kPgxW13;
+}
+
+#ifndef DPAC_PG_SEG_MAX_BLOCKS
+#define DPAC_PG_SEG_MAX_BLOCKS 1024  // every layer in one launch up to this many workgroups in all
+#endif
+// Round 6: when every layer runs on the 8-wavefront split-fp16 kernel and their grids together
+// stay small (the critic's V network over 3 B rows: 168 workgroups), one k_param_grads_x3_seg
+// launch runs them side by side (measured per layer, the four launches were latency-bound:
+// 17-28 us each on 24-48 workgroups).  DPAC_PG_SEG=0 keeps one launch per layer (tests compare
+// the two bit for bit).
+inline bool pg_seg_build(const PgArgs<float>& a, int64_t nch, PgxSegs& sg, int& smem) {
+  const char* e = getenv("DPAC_PG_SEG");  // read per launch
+  if (e && e[0] == '0') return false;
+  if (a.L + 1 > (int)(sizeof(sg.s) / sizeof(sg.s[0]))) return false;
+  sg.n = 0;
+  smem = 0;
+  int64_t b0 = 0;
+  for (int l = 0; l <= a.L; ++l) {
+    const int K = a.width[l], H = a.width[l + 1];
+    const bool x3ok = l == 0 ? (K <= 32 && H > 32) : (H <= 32 || K <= 208);
+    if (!x3ok || pgx_w_ok(a, l)) return false;
+    int ngrp = 1;
+    const int cfg = x3_layer_cfg(a, l, ngrp);
+    if (!pgx_seg_cfg_ok(cfg)) return false;
+    sg.s[sg.n++] = PgxSeg{l, cfg, ngrp, b0};
+    b0 += nch * ngrp;
+    smem = std::max(smem, pgx_cfg_smem(cfg));
+  }
+  return b0 <= DPAC_PG_SEG_MAX_BLOCKS;
+}
+
 constexpr int64_t kFallbackBlocksPg = 256;  // the guarded f32 parameter-gradient fallback's grid
 
 template <typename T>
@@ -308,7 +357,19 @@ int launch(int64_t rows, const dpac_mlp& net, double gamma_scale, const void* x,
         a.status = net.status;
         const int64_t nch = (rows + a.rows_per_chunk - 1) / a.rows_per_chunk;
         const bool fb_only = net.guard_phase == DPAC_GUARD_FALLBACK_ONLY;
-        for (int l = 0; l <= a.L && !fb_only; ++l) {
+        PgxSegs sg;
+        int seg_smem = 0;
+        const bool seg = !fb_only && pg_seg_build(a, nch, sg, seg_smem);
+        if (seg) {
+          auto k = k_param_grads_x3_seg;
+          if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, seg_smem))
+            return (int)e;
+          const int64_t nb = sg.s[sg.n - 1].b0 + nch * sg.s[sg.n - 1].ngrp;
+          hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(64 * kPgxWaves), seg_smem, s0, a, sg);
+          if (hipError_t e = hipGetLastError()) return (int)e;
+        }
+        for (int l = 0; l <= a.L && !fb_only && !seg; ++l) {
           // a run of adjacent layers of the merged-group kernel's 13-tile bin (the wide hidden
           // layers, and the output layer after them): one launch (k_param_grads_x3w, lsel < 0)
           // (and the input layer before them, run by the same kernel at run time)

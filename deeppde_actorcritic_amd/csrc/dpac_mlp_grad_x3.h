@@ -96,8 +96,11 @@ struct PgxPlan {
   static constexpr int kSmem = kMain + (4 * CW + 2 * CW) * 4;
 };
 
+// One workgroup's work: chunk `chunk` of the rows, column group `grp` of layer l (the kernel
+// k_param_grads_x3 below with its block indices; k_param_grads_x3_seg runs several layers'
+// grids in one launch).
 template <int NTI, int NTJ, int WI, bool L0, int NW = kPgxWaves>
-__global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> a, const int l) {
+__device__ __forceinline__ void pgx_body(const PgArgs<float>& a, const int l, const int64_t chunk, const int grp) {
   using PL = PgxPlan<NTI, NTJ, WI, L0, NW>;
   constexpr int WJ = PL::WJ, CW = PL::CW, KP = PL::KP, QA = PL::QA, QB = PL::QB, FL = PL::FL;
   static_assert(CW <= 256 && KP <= DPAC_MLP_MAX_WIDTH, "staging map: 256 columns, 256 features");
@@ -111,7 +114,6 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
   int* const s_cexp = reinterpret_cast<int*>(s_cfac + CW);
   if (x3_status_set(a.status)) return;  // fell back: the f32 kernel after this one does the work
   bool bad = false;  // a split operand outside the range (dpac.h dpac_mlp.status)
-  const int grp = blockIdx.y;
   const int K = a.width[l], H = a.width[l + 1];
   const int col0 = grp * CW;
   if (col0 >= H) return;  // whole workgroup, before any barrier
@@ -122,7 +124,6 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
   static_assert(FL % 64 == 0, "a wave's lanes share one row block");
   const int rbu = __builtin_amdgcn_readfirstlane(rb);
   (void)rbu;
-  const int64_t chunk = blockIdx.x;
   const int64_t r_begin = chunk * a.rows_per_chunk;
   const int64_t r_end = min(a.rows, r_begin + a.rows_per_chunk);
   const bool first = L0 && grp == 0;  // also sums BN_0 (L0: l == 0)
@@ -426,6 +427,78 @@ __global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> 
 // Requires 16-byte aligned rows: ztot, zoff[l], zoff[l+1] multiples of 4 (launch() checks).
 constexpr int kPgwThreads = 1024;
 constexpr int kPgwCW = 256;
+template <int NTI, int NTJ, int WI, bool L0, int NW = kPgxWaves>
+__global__ __launch_bounds__(64 * NW) void k_param_grads_x3(const PgArgs<float> a, const int l) {
+  pgx_body<NTI, NTJ, WI, L0, NW>(a, l, blockIdx.x, blockIdx.y);
+}
+
+// Several layers' grids of the 8-wavefront split-fp16 kernel in ONE launch (round 6): segment
+// i runs layer s[i].l with configuration s[i].cfg over blocks [s[i].b0, s[i].b0 + nch * ngrp),
+// chunk-major.  For small row counts (the critic's V network over 3 B rows: 24 chunks) each
+// layer's grid covers a fraction of the CUs and its launch is latency-bound, so the layers run
+// side by side instead of one after another; every layer writes its own partial columns.
+enum PgxCfg : int {
+  kPgxIn1 = 0, kPgxIn2, kPgxW1, kPgxW2, kPgxW4, kPgxW8, kPgxW13, kPgxN11, kPgxN12, kPgxN21, kPgxN22, kPgxNCfg
+};
+struct PgxSeg {
+  int l, cfg, ngrp;
+  int64_t b0;
+};
+struct PgxSegs {
+  int n;
+  PgxSeg s[DPAC_MLP_MAX_HIDDEN + 1];
+};
+template <int CFG>
+struct PgxCfgT;
+template <> struct PgxCfgT<kPgxIn1> { using PL = PgxPlan<1, 1, 1, true, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxIn2> { using PL = PgxPlan<2, 1, 1, true, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxW1> { using PL = PgxPlan<1, 1, 1, false, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxW2> { using PL = PgxPlan<2, 1, 1, false, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxW4> { using PL = PgxPlan<4, 1, 1, false, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxW8> { using PL = PgxPlan<8, 1, 1, false, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxW13> { using PL = PgxPlan<13, 1, 1, false, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxN11> { using PL = PgxPlan<1, 1, 8, false, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxN12> { using PL = PgxPlan<1, 2, 8, false, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxN21> { using PL = PgxPlan<2, 1, 8, false, kPgxWaves>; };
+template <> struct PgxCfgT<kPgxN22> { using PL = PgxPlan<2, 2, 8, false, kPgxWaves>; };
+// the configurations k_param_grads_x3_seg runs
+inline bool pgx_seg_cfg_ok(int cfg) {
+  return cfg == kPgxIn1 || cfg == kPgxIn2 || cfg == kPgxW13 || cfg == kPgxN11 || cfg == kPgxN21;
+}
+// the dynamic LDS of a configuration (host)
+inline int pgx_cfg_smem(int cfg) {
+  switch (cfg) {
+    case kPgxIn1: return PgxCfgT<kPgxIn1>::PL::kSmem;
+    case kPgxIn2: return PgxCfgT<kPgxIn2>::PL::kSmem;
+    case kPgxW1: return PgxCfgT<kPgxW1>::PL::kSmem;
+    case kPgxW2: return PgxCfgT<kPgxW2>::PL::kSmem;
+    case kPgxW4: return PgxCfgT<kPgxW4>::PL::kSmem;
+    case kPgxW8: return PgxCfgT<kPgxW8>::PL::kSmem;
+    case kPgxW13: return PgxCfgT<kPgxW13>::PL::kSmem;
+    case kPgxN11: return PgxCfgT<kPgxN11>::PL::kSmem;
+    case kPgxN12: return PgxCfgT<kPgxN12>::PL::kSmem;
+    case kPgxN21: return PgxCfgT<kPgxN21>::PL::kSmem;
+    default: return PgxCfgT<kPgxN22>::PL::kSmem;
+  }
+}
+
+__global__ __launch_bounds__(64 * kPgxWaves) void k_param_grads_x3_seg(const PgArgs<float> a, const PgxSegs sg) {
+  const int64_t b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < sg.n && b >= sg.s[i + 1].b0) ++i;  // segments in block order
+  const PgxSeg& g = sg.s[i];
+  const int64_t r = b - g.b0;
+  const int64_t chunk = r / g.ngrp;
+  const int grp = (int)(r - chunk * g.ngrp);
+  switch (g.cfg) {  // the critic V network's shapes (pgx_seg_cfg_ok); more cases spill
+    case kPgxIn1: pgx_body<1, 1, 1, true>(a, g.l, chunk, grp); break;
+    case kPgxIn2: pgx_body<2, 1, 1, true>(a, g.l, chunk, grp); break;
+    case kPgxW13: pgx_body<13, 1, 1, false>(a, g.l, chunk, grp); break;
+    case kPgxN11: pgx_body<1, 1, 8, false>(a, g.l, chunk, grp); break;
+    default: pgx_body<2, 1, 8, false>(a, g.l, chunk, grp); break;
+  }
+}
+
 template <int NTI, bool L0 = false>
 struct PgwPlan {
   static constexpr int KP = 16 * NTI;

@@ -89,7 +89,13 @@ __device__ uint32_t g_x3_trace[256 * 8 * 16];  // [block][wave][point]
 #endif
 
 #ifndef DPAC_X3_SPF
-#define DPAC_X3_SPF 2  // chunks of weights in flight ahead of the one being multiplied
+#define DPAC_X3_SPF 2  // chunks of weights in flight ahead of the one being multiplied (forward)
+#endif
+#ifndef DPAC_X3_SPF_BWD
+#define DPAC_X3_SPF_BWD 2  // the same for the backward chain
+#endif
+#ifndef DPAC_X3_MASK_EARLY
+#define DPAC_X3_MASK_EARLY 1  // the backward's sign-bit word loaded before the K loop (1) or after it (0)
 #endif
 
 __device__ __forceinline__ void x3_split(float a, _Float16& hi, _Float16& lo) {
@@ -158,7 +164,7 @@ __device__ __forceinline__ x3f4 x3_load4(__amdgpu_buffer_rsrc_t r, const float* 
 // = ceil(K / 32) as a template constant (straight-line code, counted waits) or 0
 // (runtime K, single-buffered).  epi.pre<NT>() runs before the K loop, epi.post<NT>()
 // after it.  Returns whether a stored operand left the split range (epi.store's result).
-template <int NT, int NCH, int RT, class EPI>
+template <int NT, int NCH, int RT, int SPF, class EPI>
 __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, const _Float16* Wx3, int wave,
                                            int lane, EPI& epi) {
   const int col_l = lane & 15, q = lane >> 4;
@@ -194,7 +200,7 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
       }
   };
   if constexpr (NCH > 0) {
-    constexpr int PF = DPAC_X3_SPF < NCH ? DPAC_X3_SPF : NCH;
+    constexpr int PF = SPF < NCH ? SPF : NCH;
     x3h8 wh[PF][NT], wl[PF][NT];
 #pragma unroll
     for (int f = 0; f < PF; ++f)
@@ -262,7 +268,7 @@ __device__ __forceinline__ bool x3_layer_t(const _Float16* in, int K, int Nout, 
   return bad;
 }
 
-template <int RT = kX3RT, class EPI>
+template <int RT = kX3RT, int SPF = DPAC_X3_SPF, class EPI>
 __device__ __forceinline__ bool x3_layer(const _Float16* in, int K, int Nout, const _Float16* Wx3, int wave,
                                          int lane, EPI& epi) {
   const int ntiles = (Nout + 15) / 16;
@@ -270,15 +276,15 @@ __device__ __forceinline__ bool x3_layer(const _Float16* in, int K, int Nout, co
   const int nch = x3_chunks(K);
   // straight-line layers for the shipped shapes (d <= 32: one chunk; 193..224 wide: seven)
   if (nch == 1) {
-    if (mine == 1) return x3_layer_t<1, 1, RT>(in, K, Nout, Wx3, wave, lane, epi);
-    if (mine == 2) return x3_layer_t<2, 1, RT>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 1) return x3_layer_t<1, 1, RT, SPF>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 2) return x3_layer_t<2, 1, RT, SPF>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (nch == 7) {
-    if (mine == 1) return x3_layer_t<1, 7, RT>(in, K, Nout, Wx3, wave, lane, epi);
-    if (mine == 2) return x3_layer_t<2, 7, RT>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 1) return x3_layer_t<1, 7, RT, SPF>(in, K, Nout, Wx3, wave, lane, epi);
+    if (mine == 2) return x3_layer_t<2, 7, RT, SPF>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (mine == 1) {
-    return x3_layer_t<1, 0, RT>(in, K, Nout, Wx3, wave, lane, epi);
+    return x3_layer_t<1, 0, RT, SPF>(in, K, Nout, Wx3, wave, lane, epi);
   } else if (mine == 2) {
-    return x3_layer_t<2, 0, RT>(in, K, Nout, Wx3, wave, lane, epi);
+    return x3_layer_t<2, 0, RT, SPF>(in, K, Nout, Wx3, wave, lane, epi);
   }
   epi.finish(lane);  // a wave without tiles: its (zero) sign-bit mask word
   return false;
@@ -430,11 +436,12 @@ struct X3BwdEpi {
     }
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) ri[rt] = rinv[rt * 16 + (lane & 15)];
+    if constexpr (!FIRST && MASKED && DPAC_X3_MASK_EARLY) mword = mp[lane] >> mshift;
   }
   template <int NT>
   __device__ __forceinline__ void post(int wave, int lane) {  // every z load, then one wait
     if constexpr (!FIRST && MASKED) {
-      mword = mp[lane] >> mshift;
+      if constexpr (!DPAC_X3_MASK_EARLY) mword = mp[lane] >> mshift;
     } else if constexpr (!FIRST) {
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
@@ -594,11 +601,10 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
   MrArgs<float> ta{};
   ta.td_x = a.td_x; ta.td_u = a.td_u; ta.td_dw = a.td_dw; ta.td_ldx = a.td_ldx; ta.td_ldu = a.td_ldu;
   ta.td_sa = a.td_sa; ta.td_sb = a.td_sb;
-  x3_zero<kX3RowsB>(img0, tid);
-  x3_zero<kX3RowsB>(img1, tid);
-  __syncthreads();
   // G_{L+1} = dL/d out, row by row (8 lanes per row): to G unscaled, and times the row's
-  // power of two 2^e (max |G_{L+1}| of the row in [1, 2)) split into image 0
+  // power of two 2^e (max |G_{L+1}| of the row in [1, 2)) split into image 0.  Round 6: for
+  // hout <= 32 (the G network's d) the loads are issued first and kept in registers, their
+  // latency under the LDS clear (rounds 3-5 loaded every element twice, after the clear).
   {
     const int r = tid / 8, sub = tid % 8;  // 8 lanes per row (kX3RowsB rows: the first 8 kX3RowsB threads)
     const bool live = r < rows_live;
@@ -612,20 +618,48 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
       return a.g_gdot ? buf_load_elem<float>(rgd, o * 4u) * td_sdw(src, gr, k)
                       : buf_load_elem<float>(rgo, (o * (uint32_t)hout + (uint32_t)k) * 4u);
     };
+    constexpr int kTopReg = 4;
+    const bool inreg = hout <= 8 * kTopReg;
+    float gv[kTopReg];
+#pragma unroll
+    for (int i = 0; i < kTopReg; ++i) {
+      const int k = sub + 8 * i;
+      gv[i] = (inreg && live && k < hout) ? g_top(k) : 0.f;
+    }
+    x3_zero<kX3RowsB>(img0, tid);
+    x3_zero<kX3RowsB>(img1, tid);
     float mx = 0.f;
-    for (int k = sub; k < hout; k += 8) {
-      const float v = live ? g_top(k) : 0.f;
-      if (live) a.G[gr * a.gtot + a.goff[L + 1] + k] = v;
-      mx = fmaxf(mx, fabsf(v));
+    if (inreg) {
+#pragma unroll
+      for (int i = 0; i < kTopReg; ++i) {
+        const int k = sub + 8 * i;
+        if (live && k < hout) a.G[gr * a.gtot + a.goff[L + 1] + k] = gv[i];
+        mx = fmaxf(mx, fabsf(gv[i]));
+      }
+    } else {
+      for (int k = sub; k < hout; k += 8) {
+        const float v = live ? g_top(k) : 0.f;
+        if (live) a.G[gr * a.gtot + a.goff[L + 1] + k] = v;
+        mx = fmaxf(mx, fabsf(v));
+      }
     }
 #pragma unroll
     for (int m = 1; m < 8; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
     int e = 0;
     if (mx > 0.f && mx < 3.0e38f) (void)frexpf(mx, &e);  // mx in [2^(e-1), 2^e)
     const float sc = ldexpf(1.f, 1 - e);                   // max |G| * sc in [1, 2)
-    for (int k = sub; k < hout; k += 8) {
-      const float v = live ? g_top(k) : 0.f;
-      if (r < kX3RowsB) bad |= x3_put(img0, r, k, v * sc);
+    __syncthreads();  // the images are clear
+    if (inreg) {
+#pragma unroll
+      for (int i = 0; i < kTopReg; ++i) {
+        const int k = sub + 8 * i;
+        if (r < kX3RowsB && k < hout) bad |= x3_put(img0, r, k, gv[i] * sc);
+      }
+    } else {
+      for (int k = sub; k < hout; k += 8) {
+        const float v = live ? g_top(k) : 0.f;
+        if (r < kX3RowsB) bad |= x3_put(img0, r, k, v * sc);
+      }
     }
     if (sub == 0 && r < kX3RowsB) rinv[r] = ldexpf(1.f, e - 1);
   }
@@ -643,12 +677,12 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) 
                                   MASKED ? a.mask + ((int64_t)(l - 1) * a.nblk + (row0 >> 6)) * kX3MaskWords + wave * 64
                                          : nullptr,
                                   8 * (int)((row0 & 63) >> 4)};
-      bad |= x3_layer<kX3RTB>(img(pq), a.width[l + 1], a.width[l], a.wx3[l], wave, lane, epi);
+      bad |= x3_layer<kX3RTB, DPAC_X3_SPF_BWD>(img(pq), a.width[l + 1], a.width[l], a.wx3[l], wave, lane, epi);
     } else {
       X3BwdEpi<true> epi{2 + 2 * L, nullptr, nullptr, rows_live, a.width[0], img(pq ^ 1), make_rsrc(nullptr, 0), 0, rg, a.gtot,
                          x3_rows_rsrc(a.g_x, row0, rows_live, a.width[0]), a.g_x != nullptr, a.scale[0], rinv,
                          nullptr, gp, a.g_x ? a.g_x + row0 * a.width[0] : nullptr, nullptr, 0};
-      x3_layer<kX3RTB>(img(pq), a.width[1], a.width[0], a.wx3[0], wave, lane, epi);  // dL/dx: not split again
+      x3_layer<kX3RTB, DPAC_X3_SPF_BWD>(img(pq), a.width[1], a.width[0], a.wx3[0], wave, lane, epi);  // dL/dx: not split again
     }
     __syncthreads();
     X3_MARK(3 + 2 * (L - l));

@@ -181,6 +181,37 @@ def test_param_grads_merged_group_kernel_bitwise(widths, R, gscale, kern, monkey
         assert torch.equal(a, c), float((a - c).abs().max())
 
 
+@pytest.mark.parametrize("widths,R", [
+    ((20, 200, 200, 200, 1), 6144),        # the lqr_d20 critic V network over 3 B rows (B = 2048)
+    ((20, 200, 200, 200, 1), 777),         # ragged: the last chunk ends inside a sub-chunk
+    ((4, 200, 200, 200, 1), 1),            # one row, a one-tile input layer
+    ((10, 150, 200, 16), 3000)])           # a 10-tile input, a 16-column output
+@pytest.mark.parametrize("gscale", [1.0, "ramp"])
+def test_param_grads_segmented_launch_bitwise(widths, R, gscale, monkeypatch):
+    """Round 6: for small row counts every layer of the 8-wavefront split-fp16 kernel runs in
+    one launch (k_param_grads_x3_seg, each workgroup on its layer's segment of the grid); the
+    gradients equal the one-launch-per-layer path (DPAC_PG_SEG=0) bit for bit."""
+    scales, shifts, Ws, b = random_net(widths, torch.float32, seed=5 * R + len(widths))
+    g = torch.Generator().manual_seed(R + 2)
+    rnd = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(torch.float32).to(DEV)
+    x, z, G = rnd(R, widths[0]), rnd(R, sum(widths[1:])), rnd(R, sum(widths))
+    if gscale == "ramp":
+        G = G * torch.logspace(-9, 0, R, dtype=torch.float64).to(torch.float32).to(DEV).unsqueeze(1)
+    view = ops.MlpView(scales, shifts, Ws, b, False, weights_x3=[_x3_image(W) for W in Ws])
+    like = scales + shifts + Ws + [b]
+    monkeypatch.delenv("DPAC_PG_X3", raising=False)
+    monkeypatch.delenv("DPAC_PG_SEG", raising=False)
+    seg = ops.mlp_param_grads(view, x, z, G, like)
+    monkeypatch.setenv("DPAC_PG_SEG", "0")
+    per_layer = ops.mlp_param_grads(view, x, z, G, like)
+    monkeypatch.setenv("DPAC_PG_X3", "0")
+    f32 = ops.mlp_param_grads(view, x, z, G, like)
+    assert any(not torch.equal(a, c) for a, c in zip(seg, f32)), "the split-fp16 kernels did not run"
+    for a, c in zip(seg, per_layer):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, c), float((a - c).abs().max())
+
+
 @pytest.mark.parametrize("kern", ["w", "d"])
 def test_param_grads_merged_group_high_address_words(kern, monkeypatch):
     """Regression test of round 4's address fault in k_param_grads_x3w (the operand rows'

@@ -63,7 +63,8 @@ def main():
             _lib.call("dpac_mlp_rows_bwd_masked", _lib.F32, R, ctypes.byref(bview.struct), ops._ptr_array(wt),
                       ops._ptr_array(wt_km), ops._ptr(z), ops._ptr(mask), ops._ptr(g), ops._ptr(G), None,
                       ops._stream(x))
-        res = {"fwd_saves": timeit(lambda: ops.mlp_rows(view, x, save=True)),
+        res = {"fwd": timeit(lambda: ops.mlp_rows(view, x, save=False)),
+               "fwd_saves": timeit(lambda: ops.mlp_rows(view, x, save=True)),
                "fwd_saves_mask": timeit(lambda: ops.mlp_rows(view, x, save=True, mask=True)),
                "fwd_td1_saves": timeit(lambda: ops.mlp_rows_td1(eqp, view, x, u, dw, save=True)),
                "fwd_td1_saves_mask": timeit(lambda: ops.mlp_rows_td1(eqp, view, x, u, dw, save=True, mask=True)),

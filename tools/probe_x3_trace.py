@@ -52,6 +52,14 @@ def main():
         _, z, m = ops.mlp_rows_td1(eqp, view, x, u, dw, save=True, mask=True)
     torch.cuda.synchronize()
     print(json.dumps({"fwd_td1": table(lib, 10)}), flush=True)
+    for _ in range(3):  # the same network without saves, mask or TD1 (what the saves cost)
+        ops.mlp_rows(view, x, save=False)
+    torch.cuda.synchronize()
+    print(json.dumps({"fwd_nosave": table(lib, 10)}), flush=True)
+    for _ in range(3):  # saves only
+        ops.mlp_rows(view, x, save=True)
+    torch.cuda.synchronize()
+    print(json.dumps({"fwd_saves": table(lib, 10)}), flush=True)
     params = [p.detach() for p in net.trainable_variables()]
     for _ in range(3):
         ops.row_mlp_backward(net.bn_rs, params, x, z, g, False, False, mask=m)
