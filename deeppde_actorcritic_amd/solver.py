@@ -382,7 +382,10 @@ class _SplitActorGraphs:
         with torch.cuda.graph(self.g_bwd, capture_error_mode=_CAPTURE_MODE):
             with defer() as self.redo_fns:
                 self.out = bwd_fn(self.fwd)
-        self.g_redo = _capture_redo(self.redo_fns)
+            if not GUARD_DEFER_JOIN:  # the fallbacks at the chain's end, in the same graph
+                for f in self.redo_fns:
+                    f()
+        self.g_redo = _capture_redo(self.redo_fns) if GUARD_DEFER_JOIN else None
 
     def launch_forward(self, batch: TrajectoryBatch):
         """On the side stream, after the work queued so far on the current stream."""
@@ -400,7 +403,8 @@ class _SplitActorGraphs:
         return list(self.out)
 
     def redo(self):
-        """The backward's deferred guard fallbacks, on the current stream."""
+        """The backward's deferred guard fallbacks, on the current stream (DPAC_GUARD_DEFER=join;
+        otherwise they ended the backward graph)."""
         if self.g_redo is not None:
             self.g_redo.replay()
 
@@ -438,7 +442,10 @@ class _SplitCriticGraphs:
         with torch.cuda.graph(self.g_back, capture_error_mode=_CAPTURE_MODE):
             with defer() as self.redo_fns:
                 self.back_out = back_fn((None,) + tuple(self.head_out[1]))
-        self.g_redo = _capture_redo(self.redo_fns)
+            if not GUARD_DEFER_JOIN:  # the fallbacks at the chain's end, on the side stream
+                for f in self.redo_fns:
+                    f()
+        self.g_redo = _capture_redo(self.redo_fns) if GUARD_DEFER_JOIN else None
 
     def head(self, batch: TrajectoryBatch):
         """The head graph on the current stream."""
@@ -461,8 +468,8 @@ class _SplitCriticGraphs:
         return list(self.back_out)
 
     def redo(self):
-        """The G backward's deferred guard fallbacks, on the current stream (after it has
-        waited for the side stream)."""
+        """The G backward's deferred guard fallbacks, on the current stream after it has waited
+        for the side stream (DPAC_GUARD_DEFER=join; otherwise they ended the backward graph)."""
         if self.g_redo is not None:
             self.g_redo.replay()
 
@@ -491,9 +498,16 @@ def graph_sets(rows: int) -> int:
 
 # DPAC_GUARD_DEFER=1 (default): the split graphs' backward chains (the actor's BPTT and its
 # parameter gradients, G's row backward and parameter gradients) launch their range-guard
-# fallbacks not behind each split-fp16 launch but together, after the two chains have joined
-# (ops.deferred_fallbacks, dpac.h guard_phase; round 6); 0: inline, as before.
-GUARD_DEFER = os.environ.get("DPAC_GUARD_DEFER", "1") != "0"
+# fallbacks not behind each split-fp16 launch but at the end of the chain, in the chain's own
+# graph on its own stream (ops.deferred_fallbacks, dpac.h guard_phase; round 6).  Each chain's
+# fallbacks follow every split-fp16 launch of that chain, so whichever launch sets the device's
+# sticky status word — this chain's or the other's — the chain is recomputed in exact f32 before
+# its gradients are read.  "join": one redo graph after the two chains have joined (round 6's
+# first form: on the critical path, ~60 us of no-op launches and graph gaps per iteration);
+# 0: inline, behind each launch (rounds 4-5).
+_GD_ENV = os.environ.get("DPAC_GUARD_DEFER", "1")
+GUARD_DEFER = _GD_ENV != "0"
+GUARD_DEFER_JOIN = _GD_ENV == "join"
 
 # DPAC_GBACK=late (default): the critic's G backward is launched on its side stream after V's
 # update and the actor's BPTT are queued, so it runs beside the BPTT and the actor's
@@ -915,8 +929,8 @@ class ActorCriticSolver(object):
         if GBACK != "early":
             gG = cg.launch_back(head_done)
         torch.cuda.current_stream().wait_stream(cg.side)  # G's gradients, made on the side stream
-        sg.redo()  # both chains' deferred range-guard fallbacks: no-ops unless a split operand overflowed
-        cg.redo()
+        sg.redo()  # DPAC_GUARD_DEFER=join: both chains' range-guard fallbacks (no-ops unless a split
+        cg.redo()  # operand overflowed); by default each chain's graph ends with its own
         g, gG = self.par.allreduce_grads_multi([(g, cnt, atot), (gG, ccnt, ctot)])
         self.optimizer_actor.apply_gradients(zip(g, self.actor_variables()))
         self.optimizer_critic.apply_gradients(zip(gG, self.model_critic.NN_value_grad.trainable_variables()))

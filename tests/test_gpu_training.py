@@ -218,8 +218,9 @@ def test_graph_sets_one_and_two_give_bitwise_equal_parameters(monkeypatch):
 
 @pytest.mark.parametrize("big", [None, 2.0 ** 20])
 def test_guard_deferred_and_inline_give_bitwise_equal_parameters(monkeypatch, big):
-    """Round 6: the backward chains' range-guard fallbacks replayed as one
-    redo graph after the actor's and G's chains join (DPAC_GUARD_DEFER=1, the default) against
+    """Round 6: the backward chains' range-guard fallbacks at the end of each
+    chain's own graph (DPAC_GUARD_DEFER=1, the default) and as one redo graph after the actor's
+    and G's chains join (join) against
     each fallback right behind its split-fp16 launch (0): bitwise the same parameters over 4
     iterations, in range (the fallbacks stay no-ops) and with every network's BN_1 times 2^20
     (the status word is set and the deferred fallbacks recompute the chains in exact f32)."""
@@ -227,4 +228,11 @@ def test_guard_deferred_and_inline_give_bitwise_equal_parameters(monkeypatch, bi
     pd, fd = _production_params(monkeypatch, "GUARD_DEFER", True, big=big)
     assert fi == fd == (big is not None)
     for a, b in zip(pi, pd):
+        _bitwise(a, b)
+    # DPAC_GUARD_DEFER=join: one redo graph after the chains join (the default ends each chain's
+    # own graph with its fallbacks)
+    monkeypatch.setattr(psol, "GUARD_DEFER_JOIN", True)
+    pj, fj = _production_params(monkeypatch, "GUARD_DEFER", True, big=big)
+    assert fj == fi
+    for a, b in zip(pi, pj):
         _bitwise(a, b)
