@@ -661,8 +661,8 @@ def main():
             if world == 1:
                 # BASELINE configs[1], [2] (B = 4096 on one GPU), configs[4]'s per-GPU shard of
                 # 65536 over 8 GPUs, and the reference's shipped batch (configs/*.json: 2048)
-                variants["training_lqr_d20"] = training_variant("lqr_d20", dtype, 2048)
-                variants["training_lqr_d20_b4096"] = training_variant("lqr_d20", dtype, 4096)
+                variants["training_lqr_d20"] = training_variant("lqr_d20", dtype, 2048, iters=30, warmup=5)
+                variants["training_lqr_d20_b4096"] = training_variant("lqr_d20", dtype, 4096, iters=20, warmup=5)
                 variants["training_ekn_d20_b4096"] = training_variant("ekn_d20", dtype, 4096)
                 variants["training_vdp_d20_b8192"] = training_variant("vdp_d20", dtype, 8192, iters=4)
             # BASELINE configs[3]: lqr_var_d20, global batch 16384 split over the ranks, one
