@@ -94,6 +94,9 @@ __device__ uint32_t g_x3_trace[256 * 8 * 16];  // [block][wave][point]
 #ifndef DPAC_X3_SPF_BWD
 #define DPAC_X3_SPF_BWD 2  // the same for the backward chain
 #endif
+#ifndef DPAC_X3_BWD_MINB
+#define DPAC_X3_BWD_MINB 1  // min waves per SIMD the backward is compiled for (launch bounds; timing knob)
+#endif
 #ifndef DPAC_X3_MASK_EARLY
 #define DPAC_X3_MASK_EARLY 1  // the backward's sign-bit word loaded before the K loop (1) or after it (0)
 #endif
@@ -584,7 +587,7 @@ __global__ __launch_bounds__(kX3Threads) void k_mlp_rows_fwd_x3(const X3Args a) 
 
 // MASKED: the activation factors from the forward's sign-bit bytes (a.mask) instead of z
 template <bool MASKED>
-__global__ __launch_bounds__(kX3Threads) void k_mlp_rows_bwd_x3(const X3Args a) {
+__global__ __launch_bounds__(kX3Threads, DPAC_X3_BWD_MINB) void k_mlp_rows_bwd_x3(const X3Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char x3_lds[];
   _Float16* const img0 = reinterpret_cast<_Float16*>(x3_lds);
   _Float16* const img1 = reinterpret_cast<_Float16*>(x3_lds + kX3ImgBytesB);
