@@ -509,6 +509,12 @@ _GD_ENV = os.environ.get("DPAC_GUARD_DEFER", "1")
 GUARD_DEFER = _GD_ENV != "0"
 GUARD_DEFER_JOIN = _GD_ENV == "join"
 
+# DPAC_SAMPLE_STREAM: "gside" (default, round 6: prefetch_samples draws on the G backward's side
+# stream, behind G's chain; 2.900 vs 2.906 ms per lqr_d20 iteration at B = 2048, and the
+# iteration then holds three of the box's four hardware queues, leaving one to RCCL's stream at
+# N > 1) or "own" (a stream of its own, rounds 4-5)
+SAMPLE_STREAM = os.environ.get("DPAC_SAMPLE_STREAM", "gside")
+
 # DPAC_GBACK=late (default): the critic's G backward is launched on its side stream after V's
 # update and the actor's BPTT are queued, so it runs beside the BPTT and the actor's
 # parameter gradients; "early": right after the critic head, beside V's backward, V's Adam
@@ -675,7 +681,13 @@ class ActorCriticSolver(object):
         if self.sampler != "device":
             return
         if self._sample_side is None:
-            self._sample_side = torch.cuda.Stream()
+            # SAMPLE_STREAM "gside": the G backward's side stream (once it exists), so a training
+            # iteration uses three streams of its own and a fourth hardware queue stays free for
+            # RCCL's stream at N > 1 (the box runs 4 queues per process)
+            if SAMPLE_STREAM == "gside" and self._side_g is not None:
+                self._sample_side = self._side_g
+            else:
+                self._sample_side = torch.cuda.Stream()
         # the next iteration's graph set (train_iteration alternates two): its static inputs are
         # drawn into in place, once the iteration that last read them is done, so the next
         # iteration copies nothing in (round 5); otherwise fresh buffers
