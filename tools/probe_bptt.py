@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--only", default="fwd,bwd,pg")
+    ap.add_argument("--eqn", default="LQR", help="LQR, VDP, EKN or LQR_var (d = 20)")
     ap.add_argument("--dump", default=None, help="save the forward's and the BPTT's outputs (torch.save) for a "
                                                  "bitwise A/B of two builds (tools/cmp_dumps.py)")
     a = ap.parse_args()
@@ -51,9 +52,9 @@ def main():
     N = a.N
     only = a.only.split(",")
     for B in [int(v) for v in a.B.split(",")]:
-        cfg = full_config("LQR", 20, N=N, hidden=(200, 200, 200), batch=B,
+        cfg = full_config(a.eqn, 20, N=N, hidden=(200, 200, 200), batch=B,
                           dtype="float32" if a.dtype == "f32" else "float64")
-        bsde = peq.LQR(cfg.eqn_config)
+        bsde = getattr(peq, a.eqn)(cfg.eqn_config)
         net = psol.DeepNN(cfg, "actor", torch.Generator().manual_seed(0), dt_, "cuda")
         eqp = bsde.params()
         x0, dw, _ = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=1, dtype=dt_, device="cuda")
@@ -80,7 +81,7 @@ def main():
                        f"{a.dump}_{B}.pt")
         pg = lambda: ops.mlp_param_grads(view, x[:N].reshape(N * B, 20), z.reshape(N * B, -1),
                                          Gall.reshape(N * B, -1), params)
-        out = {"B": B, "N": N, "dtype": a.dtype}
+        out = {"eqn": a.eqn, "B": B, "N": N, "dtype": a.dtype}
         flop = MLP_FLOP_PER_ROW * B * N
         for name, fn, fl in (("fwd", fwd, flop), ("bwd", bwd, flop), ("pg", pg, flop)):
             if name not in only:
