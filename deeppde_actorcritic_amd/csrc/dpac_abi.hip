@@ -197,7 +197,7 @@ int launch(const OpArgs& a) {
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int64_t b0, int nb, int N, int D, int sample_type,
-                                                   uint64_t seed, int64_t traj_offset, T* dw) {
+                                                   uint64_t seed, int64_t traj_offset, T* dw, bool pairs8) {
   // thread (unit u, trajectory b0 + bl, lane slot p, block): the stream layout of draw_slot(); a
   // unit is a step pair in the paired layout (S = 2), else one step.  x runs over this launch's
   // (bl, p, block) in 32-bit arithmetic, y over the units with a stride (round 6: the index
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void k_sample_dw(int64_t B, int64_t b0, int nb
   // two components per lane slot and step, d even, four values a block (f32 d = 20): each step's
   // pair is one 8-byte store
   if constexpr (sizeof(T) == 4) {
-    if (S == 2 && M == 2 && PB == 4 && (D & 1) == 0) {
+    if (pairs8 && S == 2 && M == 2 && PB == 4 && (D & 1) == 0) {  // pairs8: dw 8-byte aligned
       if (jj[0] < 0) return;
       for (int u = blockIdx.y; u < units; u += gridDim.y) {
         T vals[4];
@@ -380,7 +380,8 @@ int sample_impl(const dpac_eqn_params* eq, int32_t sample_type, int64_t B, int32
       const int64_t gx = ((int64_t)nb * per_b + 255) / 256;
       const int gy = (int)std::min<int64_t>(units, std::max<int64_t>(16, (4096 + gx - 1) / gx));
       const dim3 g((unsigned)gx, (unsigned)gy);
-      hipLaunchKernelGGL(k_sample_dw<T>, g, dim3(256), 0, s, B, b0, nb, N, D, st, seed, off, (T*)dw);
+      const bool pairs8 = (reinterpret_cast<uintptr_t>(dw) & 7) == 0;  // a caller's odd-float view: scalar stores
+      hipLaunchKernelGGL(k_sample_dw<T>, g, dim3(256), 0, s, B, b0, nb, N, D, st, seed, off, (T*)dw, pairs8);
       if (hipError_t e = hipGetLastError()) return (int)e;
     }
     if (hipError_t e = hipGetLastError()) return (int)e;

@@ -203,6 +203,22 @@ def test_sampler_distribution_and_sharding(dtype):
     assert torch.all(x00 == torch.tensor(0.01, dtype=dtype))
 
 
+def test_sampler_into_a_view_that_is_not_8_byte_aligned():
+    """Round 6: the f32 sampler writes a step's two components of a lane slot as one 8-byte store
+    when dw is 8-byte aligned; a caller's view starting at an odd float (legal for the C ABI) takes
+    the scalar stores and gets the same numbers."""
+    eqp = pe(eqn_config("LQR", 20)).params()
+    B, N, d = 300, 7, 20
+    x0, dw, xb = ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=3, traj_offset=11, device=DEV)
+    buf = torch.zeros(N * B * d + 1, device=DEV)
+    dw_odd = buf[1:].view(N, B, d)
+    assert dw_odd.data_ptr() % 8 == 4
+    out = (torch.empty_like(x0), dw_odd, torch.empty_like(xb))
+    ops.sample(eqp, _lib.SAMPLE_NORMAL, B, N, seed=3, traj_offset=11, device=DEV, out=out)
+    assert torch.equal(dw_odd, dw) and torch.equal(out[0], x0) and torch.equal(out[2], xb)
+    assert float(buf[0]) == 0.0  # nothing written before the view
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("d", [1, 3, 5, 20, 33, 200])
 @pytest.mark.parametrize("sample_type", [_lib.SAMPLE_NORMAL, _lib.SAMPLE_ZERO_X0])
